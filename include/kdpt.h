@@ -1,0 +1,232 @@
+/*
+ * kdpt.h -- C-ABI drop-in boundary of the MI355X (gfx950) KD-tree path tracer.
+ *
+ * Replaces the reference's device entry points (src/pathtrace.h:6-21):
+ *   pathtraceInit(Scene*, bool enablekd)   -> kdpt_create
+ *   pathtrace(uchar4* pbo, int frame, int iter, ...13 flags)
+ *                                          -> kdpt_trace_iteration (+ kdpt_read_image,
+ *                                             kdpt_write_pbo for the uchar4 preview)
+ *   pathtraceFree(Scene*, bool enablekd)   -> kdpt_destroy
+ * Plain POD in, host pointers in, no HIP/torch types.  Every entry point returns
+ * an int status (KDPT_OK == 0) instead of exit(1) (src/pathtrace.cu:42-60);
+ * kdpt_last_error() gives the message.  One context per device; a context is
+ * not re-entrant (like the reference's file-static device globals,
+ * src/pathtrace.cu:92-98).
+ *
+ * The structs keep the reference's byte layouts so the
+ * arrays the reference's host code builds (Scene::newNodesBare,
+ * Scene::newTrianglesBare, Scene::geoms, Scene::materials) pass through as is.
+ */
+#ifndef KDPT_H
+#define KDPT_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define KDPT_OK 0
+#define KDPT_ERR_ARG -1
+#define KDPT_ERR_HIP -2
+#define KDPT_ERR_UNSUPPORTED -3
+#define KDPT_ERR_IO -4
+
+/* struct Geom, src/sceneStructs.h:22-31 (236 bytes, glm::mat4 column-major) */
+typedef struct kdpt_geom {
+    int type; /* enum GeomType: 0 SPHERE, 1 CUBE */
+    int materialid;
+    float translation[3];
+    float rotation[3];
+    float scale[3];
+    float transform[16];
+    float inverseTransform[16];
+    float invTranspose[16];
+} kdpt_geom;
+
+/* struct Material, src/sceneStructs.h:33-44 (56 bytes) */
+typedef struct kdpt_material {
+    float color[3];
+    float specular_exponent;
+    float specular_color[3];
+    float hasReflective;
+    float hasRefractive;
+    float indexOfRefraction;
+    float emittance;
+    float transmittance[3];
+} kdpt_material;
+
+/* struct Camera, src/sceneStructs.h:46-55 (84 bytes) */
+typedef struct kdpt_camera {
+    int resolution[2];
+    float position[3];
+    float lookAt[3];
+    float view[3];
+    float up[3];
+    float right[3];
+    float fov[2];
+    float pixelLength[2];
+} kdpt_camera;
+
+/* KDN::NodeBare, src/KDnode.h:64-82 (64 bytes) */
+typedef struct kdpt_node_bare {
+    int axis;
+    float splitPos;
+    float mins[3];
+    float maxs[3];
+    int ID;
+    int parentID;
+    int leftID;
+    int rightID;
+    int triIdStart;
+    int triIdSize;
+    float tmin;
+    float tmax;
+} kdpt_node_bare;
+
+/* KDN::TriBare, src/KDnode.h:51-62 (76 bytes) */
+typedef struct kdpt_tri_bare {
+    float x1, x2, x3, y1, y2, y3, z1, z2, z3;
+    float nx1, nx2, nx3, ny1, ny2, ny3, nz1, nz2, nz3;
+    int mtlIdx;
+} kdpt_tri_bare;
+
+/* struct PathSegment (+ Ray), src/sceneStructs.h:15-20,65-71 (56 bytes) */
+typedef struct kdpt_path_segment {
+    float origin[3];
+    float direction[3];
+    uint8_t isinside;
+    uint8_t pad_[3];
+    float sdepth;
+    float color[3];
+    int pixelIndex;
+    int remainingBounces;
+    int materialIdHit;
+} kdpt_path_segment;
+
+/* struct ShadeableIntersection, src/sceneStructs.h:81-85 (20 bytes) */
+typedef struct kdpt_shadeable_intersection {
+    float t;
+    float surfaceNormal[3];
+    int materialId;
+} kdpt_shadeable_intersection;
+
+/* Everything pathtraceInit reads from Scene (src/pathtrace.cu:201-272). */
+typedef struct kdpt_scene {
+    kdpt_camera camera;        /* hst_scene->state.camera (after runCuda's camera update) */
+    int traceDepth;            /* hst_scene->state.traceDepth */
+    const kdpt_geom *geoms;
+    int num_geoms;
+    const kdpt_material *materials;
+    int num_materials;
+    int has_obj;               /* hst_scene->hasObj */
+    const kdpt_node_bare *nodes; /* hst_scene->newNodesBare (ID order) */
+    int num_nodes;
+    const kdpt_tri_bare *tris; /* hst_scene->newTrianglesBare */
+    int num_tris;
+    const int *obj_materialOffsets; /* one per OBJ shape */
+    int num_shapes;
+} kdpt_scene;
+
+/* The flags of pathtrace() with src/main.cpp:35-60 defaults (kdpt_default_options). */
+typedef struct kdpt_options {
+    float focal_length;  /* dofDistance, 6 */
+    float dof_angle;     /* dofAngle, 0 */
+    float softness;      /* 0 */
+    int cacherays;       /* 0: regenerate camera rays every iteration */
+    int antialias;       /* 1 */
+    int enable_sss;      /* 0 */
+    int testing_mode;    /* 0: 1 = also time the intersect kernel per bounce (TESTINGMODE) */
+    int compaction;      /* 1 */
+    int enable_kd;       /* 1 (0 = brute force, not built: KDPT_ERR_UNSUPPORTED) */
+    int viz_kd;          /* 0 (box visualisation, not built) */
+    int use_bbox;        /* 0 */
+    int short_stack;     /* 1: traverseKDbareShortHybrid, 0: traverseKDbare */
+    int bounce_cap;      /* 8 == `depth > 7` (src/pathtrace.cu:2608); 16 for the stress config */
+    int block_size;      /* 0 = default (256) */
+    float *external_image; /* optional device float[3*W*H] to accumulate into (e.g. an RCCL buffer) */
+} kdpt_options;
+
+typedef struct kdpt_stats {
+    long long segments;          /* sum over bounces of paths launched into the intersect kernel */
+    long long seg_per_bounce[32];
+    int bounces;                 /* bounces launched in the last iteration */
+    int iterations;              /* iterations traced since create/reset */
+    float ms_last_iteration;     /* hipEvent time of the last kdpt_trace_iteration (gen .. last gather) */
+    float ms_intersect;          /* testing_mode: sum of intersect-kernel time, last iteration */
+    long long total_segments;    /* since create/reset */
+} kdpt_stats;
+
+typedef struct kdpt_ctx kdpt_ctx;
+
+void kdpt_default_options(kdpt_options *opt);
+
+/* pathtraceInit: allocate + upload (geoms, materials, nodes, triangles, offsets). */
+int kdpt_create(const kdpt_scene *scene, const kdpt_options *opt, int device, kdpt_ctx **out);
+/* pathtrace(pbo, frame, iter, ...): one iteration (1 sample per pixel); iter is 1-based and
+ * seeds the RNG.  Synchronous on return, like the reference. */
+int kdpt_trace_iteration(kdpt_ctx *ctx, int frame, int iter);
+/* As kdpt_trace_iteration but returns after enqueueing (no host sync, no stats). */
+int kdpt_trace_iteration_async(kdpt_ctx *ctx, int frame, int iter);
+int kdpt_synchronize(kdpt_ctx *ctx);
+/* The float3 accumulation image (sum over iterations, not averaged): 3*W*H floats. */
+int kdpt_read_image(kdpt_ctx *ctx, float *rgb);
+/* sendImageToPBO (src/pathtrace.cu:69-89) into host uchar4[W*H] (x,y,z,w bytes). */
+int kdpt_write_pbo(kdpt_ctx *ctx, int iter, uint8_t *rgba);
+int kdpt_reset(kdpt_ctx *ctx);
+int kdpt_get_stats(kdpt_ctx *ctx, kdpt_stats *st);
+int kdpt_destroy(kdpt_ctx *ctx);
+const char *kdpt_last_error(void);
+
+/* Device pointer of the accumulation image (for an in-place RCCL reduce). */
+int kdpt_image_device_ptr(kdpt_ctx *ctx, void **dptr);
+/* Debug / parity: run iteration `iter` through bounce `stop_depth` (0-based) and copy the
+ * live PathSegment array (reference layout) to host `out` (>= W*H entries). */
+int kdpt_debug_paths(kdpt_ctx *ctx, int iter, int stop_depth, kdpt_path_segment *out, int *npaths);
+/* Roofline counters: one extra, untimed iteration that also counts AABB tests, triangle
+ * tests and triangle hits (aabb_tri_hit[3]); the image is not touched. */
+int kdpt_count_iteration(kdpt_ctx *ctx, int iter, unsigned long long *aabb_tri_hit);
+/* Device-math known answers: sinf/cosf/pow-5 Fresnel/u01 evaluated by the gfx950 code. */
+int kdpt_selftest_math(const float *x, int n, float *sin_out, float *cos_out);
+int kdpt_selftest_rng(const int *iter_idx_depth, int n, int k, float *u_out);
+int kdpt_selftest_fresnel(const float *cosines, int n, float ior, float *f_out);
+
+/* ---- Host scene building (C++ restatement of the reference's host code) ---- */
+typedef struct kdpt_scene_data kdpt_scene_data;
+
+/* Scene text (src/scene.cpp:7-271) + optional OBJ (src/scene.cpp:579-968, tinyobjloader)
+ * + the runCuda camera (src/main.cpp:1059-1073,1111-1129).  Overrides <= 0 keep the file
+ * values; a resolution override recomputes pixelLength with the loadCamera formula. */
+int kdpt_scene_load(const char *scene_path, const char *obj_path, int res_w, int res_h, int depth,
+                    kdpt_scene_data **out);
+
+/* The same from already-parsed values (what the parsers produce; fixtures use this). */
+typedef struct kdpt_scene_desc {
+    int res[2];
+    float fovy;
+    int iterations;
+    int traceDepth;
+    float eye[3], lookAt[3], up[3];
+    int num_materials;
+    const kdpt_material *materials;
+    int num_geoms;
+    const int *geom_type;
+    const int *geom_material;
+    const float *geom_trs;          /* per geom: translation[3], rotation[3], scale[3] */
+    int ntri;                       /* 0: no OBJ */
+    const float *verts9, *norms9;   /* per triangle, vertex-index-gathered normals */
+    const int *shape_of_tri;
+    int num_shapes;
+    const kdpt_material *shape_materials;
+    int kd_max_depth;               /* 0 = 13, the reference's split(13) */
+} kdpt_scene_desc;
+int kdpt_scene_build(const kdpt_scene_desc *desc, kdpt_scene_data **out);
+/* View of the built scene as the C-ABI struct (pointers owned by the scene data). */
+int kdpt_scene_view(const kdpt_scene_data *sd, kdpt_scene *out);
+int kdpt_scene_free(kdpt_scene_data *sd);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* KDPT_H */

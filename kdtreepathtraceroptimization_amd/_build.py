@@ -1,0 +1,61 @@
+"""Build the gfx950 shared library ``libkdpt.so`` in-tree (hipcc + g++).
+
+The product is one C-ABI library (include/kdpt.h): HIP kernels + runtime
+(csrc/kdpt_runtime.hip) and the host scene builder (csrc/scene_host.cpp).
+Numerics flags are part of the contract: ``-ffp-contract=off`` and no
+fast-math on both the device and the host side, so that every float/double
+operation is the one the reference spells ("Hard parts").
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+import sys
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+ROOT = os.path.dirname(HERE)
+CSRC = os.path.join(HERE, "csrc")
+LIB = os.path.join(HERE, "libkdpt.so")
+BUILD = os.path.join(ROOT, "build")
+
+HIPCC = os.environ.get("HIPCC", "/opt/rocm/bin/hipcc")
+ARCH = os.environ.get("KDPT_ARCH", "gfx950")
+
+COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-I", os.path.join(ROOT, "include")]
+
+
+def _run(cmd):
+    print("+", " ".join(cmd), flush=True)
+    subprocess.run(cmd, check=True)
+
+
+def _sources():
+    return [os.path.join(CSRC, f) for f in sorted(os.listdir(CSRC))] + [os.path.join(ROOT, "include", "kdpt.h")]
+
+
+def up_to_date() -> bool:
+    if not os.path.exists(LIB):
+        return False
+    t = os.path.getmtime(LIB)
+    return all(os.path.getmtime(s) <= t for s in _sources())
+
+
+def build(force: bool = False, verbose_resources: bool = False) -> str:
+    if not force and up_to_date():
+        return LIB
+    os.makedirs(BUILD, exist_ok=True)
+    host_obj = os.path.join(BUILD, "scene_host.o")
+    dev_obj = os.path.join(BUILD, "kdpt_runtime.o")
+    _run(["g++", *COMMON, "-c", os.path.join(CSRC, "scene_host.cpp"), "-o", host_obj])
+    extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose_resources else []
+    _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, *extra, "-c", os.path.join(CSRC, "kdpt_runtime.hip"), "-o", dev_obj])
+    tmp = LIB + ".tmp"
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, dev_obj, host_obj])
+    os.replace(tmp, LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    build(force="--force" in sys.argv, verbose_resources="--resources" in sys.argv)
+    print(LIB)

@@ -1,0 +1,941 @@
+// kdpt_runtime.hip -- gfx950 kernels and the C-ABI (include/kdpt.h) for the
+// reference's per-sample hot path (src/pathtrace.cu:2405-2635 `pathtrace`).
+//
+// One iteration = k_gen_rays, then per bounce (cap 8, src/pathtrace.cu:2608):
+//   k_bounce   : intersect (6 analytic geoms + KD traversal) + scatterRay +
+//                shadeMaterial + partialGather fused, one lane per live path;
+//                writes the updated path in place and the tile's survivor count
+//   k_scan     : exclusive scan of tile counts (key-major when iter == 2 sorts)
+//   k_scatter  : stable compaction (thrust::remove_if) -- and on iter 2 the
+//                stable sort by materialIdHit (thrust::sort, a merge sort) --
+//                into the other path buffer.
+// No host synchronisation inside an iteration: the live-path count lives on
+// the device and kernels past the end of the live range exit at once.
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/kdpt.h"
+#include "kdpt_device.h"
+
+using namespace kdpt;
+
+namespace {
+
+constexpr int TILE = 256;  // paths per workgroup (4 waves of 64)
+constexpr int MAX_KEYS = 64;
+
+thread_local std::string g_last_error;
+
+int fail(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+#define HIP_TRY(expr)                                                                      \
+  do {                                                                                     \
+    hipError_t e_ = (expr);                                                                \
+    if (e_ != hipSuccess)                                                                  \
+      return fail(KDPT_ERR_HIP, std::string(#expr) + ": " + hipGetErrorString(e_));        \
+  } while (0)
+
+// Path state, structure of arrays of float4 (coalesced 1 KiB per wave load):
+//   p0 = {origin.xyz, sdepth}
+//   p1 = {direction.xyz, pixelIndex | isinside << 31}
+//   p2 = {color.rgb, remainingBounces}
+//   pm = materialIdHit
+struct PathBuf {
+  float4* p0;
+  float4* p1;
+  float4* p2;
+  int* pm;
+};
+
+struct Counters {
+  unsigned long long aabb, tri, hit;
+};
+
+__device__ inline unsigned int lane_prefix(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
+
+// ---------------------------------------------------------------------------
+// generateRayFromCamera (src/pathtrace.cu:315-397)
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int traceDepth, PathBuf out,
+                                                  float focalLength, float dofAngle, int antialias, int* counts,
+                                                  int ncounts) {
+  const int W = cam.resolution[0], H = cam.resolution[1];
+  const int index = blockIdx.x * blockDim.x + threadIdx.x;
+  if (index == 0) {
+    counts[0] = W * H;
+    for (int k = 1; k < ncounts; k++) counts[k] = 0;
+  }
+  if (index >= W * H) return;
+  const int x = index % W, y = index / W;
+  const f3 view = mk3(cam.view[0], cam.view[1], cam.view[2]);
+  const f3 right = mk3(cam.right[0], cam.right[1], cam.right[2]);
+  const f3 upv = mk3(cam.up[0], cam.up[1], cam.up[2]);
+  Ray ray;
+  ray.origin = mk3(cam.position[0], cam.position[1], cam.position[2]);
+  ray.isinside = false;
+  // cam.right * cam.pixelLength.x * (...): (vec * float) * float
+  f3 a = scl(scl(right, cam.pixelLength[0]), ((float)x - (float)W * 0.5f));
+  f3 b = scl(scl(upv, cam.pixelLength[1]), ((float)y - (float)H * 0.5f));
+  ray.direction = normalize(sub(sub(view, a), b));
+  Rng rng = rng_seed(utilhash((uint32_t)iter));  // same stream for every pixel (:334)
+  if (antialias) {
+    const float jitterscale = (float)0.002;
+    float j0 = u01(rng), j1 = u01(rng), j2 = u01(rng);
+    f3 v3a = normalize(mk3(j0, j1, j2));
+    ray.direction = add(ray.direction, scl(v3a, jitterscale));
+    ray.direction = normalize(ray.direction);
+  }
+  float u = kdpt_cosf(PI_F * u01(rng));
+  float u2 = u * u;
+  float sq = sqrtf(1 - u2);
+  float theta = 2 * PI_F * u01(rng);
+  f3 vv = normalize(mk3(sq * kdpt_cosf(theta), sq * kdpt_sinf(theta), u));
+  (void)u01(rng);  // R1
+  (void)u01(rng);  // R2
+  float randangle = u01(rng) * PI_F * dofAngle;
+  float qw = kdpt_cosf(randangle / 2.0f);
+  float sh = kdpt_sinf(randangle / 2.0f);
+  f3 qv = mk3(vv.x * sh, vv.y * sh, vv.z * sh);
+  // glm quat * vec3 (gtc/quaternion.inl:319-326)
+  f3 uv = cross(qv, ray.direction);
+  f3 uuv = cross(qv, uv);
+  f3 randrot = add(ray.direction, scl(add(scl(uv, qw), uuv), 2.0f));
+  ray.origin = sub(add(ray.origin, scl(ray.direction, focalLength)), scl(randrot, focalLength));
+  ray.direction = normalize(randrot);
+  out.p0[index] = make_float4(ray.origin.x, ray.origin.y, ray.origin.z, 0.0f);
+  out.p1[index] = make_float4(ray.direction.x, ray.direction.y, ray.direction.z, ibits(index));
+  out.p2[index] = make_float4(1.0f, 1.0f, 1.0f, ibits(traceDepth));
+}
+
+// ---------------------------------------------------------------------------
+// pathTraceOneBounceKDbare + shadeMaterial + partialGather (fused)
+// ---------------------------------------------------------------------------
+struct BounceArgs {
+  DevScene S;
+  PathBuf paths;
+  float* image;
+  const int* counts;
+  int depth;
+  int iter;
+  float softness;
+  int enable_sss;
+  int* tile_counts;  // [ntiles] or key-major [MAX_KEYS][ntiles] when sorting
+  int ntiles;
+  int nkeys;
+  Counters* counters;
+};
+
+template <bool HYBRID, bool COMPACT, bool SORT, bool COUNT>
+__global__ __launch_bounds__(TILE) void k_bounce(BounceArgs A) {
+  const int n = A.counts[A.depth];
+  const int tile = blockIdx.x;
+  if (tile * TILE >= n) return;  // uniform per block
+  const int i = tile * TILE + threadIdx.x;
+  __shared__ int s_hist[MAX_KEYS];
+  __shared__ unsigned int s_cnt[3];
+  if (SORT) {
+    for (int k = threadIdx.x; k < MAX_KEYS; k += TILE) s_hist[k] = 0;
+  }
+  if (COUNT && threadIdx.x < 3) s_cnt[threadIdx.x] = 0;
+  if (SORT || COUNT) __syncthreads();
+  bool alive = false;
+  int key = 0;
+  TraverseCounters cnt{0, 0, 0};
+  if (i < n) {
+    const float4 q0 = A.paths.p0[i];
+    const float4 q1 = A.paths.p1[i];
+    float4 q2 = A.paths.p2[i];
+    const int pw = fbits(q1.w);
+    const int pix = pw & 0x7fffffff;
+    Ray ray;
+    ray.origin = mk3(q0.x, q0.y, q0.z);
+    ray.direction = mk3(q1.x, q1.y, q1.z);
+    ray.isinside = (pw >> 31) & 1;
+    ray.sdepth = q0.w;
+    f3 color = mk3(q2.x, q2.y, q2.z);
+    int bounces = fbits(q2.w);
+    int matHit = A.paths.pm[i];
+    bool wrote = false;
+    if (bounces > 0) {
+      const DevScene& S = A.S;
+      Hit h;
+      h.t_min = FLT_MAXV;
+      h.hit_geom_index = -1;
+      h.obj_intersect = false;
+      h.objMaterialIdx = -1;
+      h.ip = mk3(0, 0, 0);
+      h.normal = mk3(0, 0, 0);
+      f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
+      float t = 0;
+      for (int g = 0; g < S.num_geoms; g++) {
+        const DevGeom& G = S.geoms[g];
+        if (G.type == 1) t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
+        else if (G.type == 0) t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+        if (t > 0.0f && h.t_min > t) {
+          h.t_min = t;
+          h.hit_geom_index = g;
+          h.ip = tmp_i;
+          h.normal = tmp_n;
+        }
+      }
+      if (S.has_obj) traverseKD<HYBRID, COUNT>(S, ray, h, S.num_materials, cnt);
+      float isect_t;
+      int isect_mat = 0;
+      if (h.hit_geom_index == -1) {
+        isect_t = -1.0f;
+      } else {
+        Rng rng = seeded_rng(A.iter, i, A.depth);
+        const int mid = h.obj_intersect ? h.objMaterialIdx : S.geoms[h.hit_geom_index].materialid;
+        matHit = mid;
+        scatterRay(ray, h.ip, h.normal, S.materials[mid], rng, A.softness);
+        isect_t = h.t_min;
+        isect_mat = mid;
+      }
+      shade(isect_t, isect_mat, S.materials, A.enable_sss != 0, ray, color, bounces);
+      wrote = true;
+    }
+    if (COMPACT && bounces == 0) {
+      // partialGather: one live path per pixel, so this read-modify-write never collides
+      float* px = A.image + 3 * (size_t)pix;
+      px[0] += color.x;
+      px[1] += color.y;
+      px[2] += color.z;
+    }
+    if (wrote) {
+      A.paths.p0[i] = make_float4(ray.origin.x, ray.origin.y, ray.origin.z, ray.sdepth);
+      A.paths.p1[i] = make_float4(ray.direction.x, ray.direction.y, ray.direction.z,
+                                  ibits(pix | ((ray.isinside ? 1 : 0) << 31)));
+      A.paths.p2[i] = make_float4(color.x, color.y, color.z, ibits(bounces));
+      A.paths.pm[i] = matHit;
+    }
+    alive = COMPACT ? (bounces != 0) : true;
+    key = matHit;
+  }
+  if (COUNT) {
+    // wave-reduce then one LDS atomic per wave
+    unsigned int a = cnt.aabb, tr = cnt.tri, hi = cnt.hit;
+    for (int off = 32; off > 0; off >>= 1) {
+      a += __shfl_down(a, off);
+      tr += __shfl_down(tr, off);
+      hi += __shfl_down(hi, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&s_cnt[0], a);
+      atomicAdd(&s_cnt[1], tr);
+      atomicAdd(&s_cnt[2], hi);
+    }
+  }
+  if (SORT) {
+    if (alive) atomicAdd(&s_hist[key], 1);
+    __syncthreads();
+    for (int k = threadIdx.x; k < A.nkeys; k += TILE) A.tile_counts[k * A.ntiles + tile] = s_hist[k];
+  } else {
+    const int c = __syncthreads_count(alive);
+    if (threadIdx.x == 0) A.tile_counts[tile] = c;
+  }
+  if (COUNT) {
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      atomicAdd(&A.counters->aabb, (unsigned long long)s_cnt[0]);
+      atomicAdd(&A.counters->tri, (unsigned long long)s_cnt[1]);
+      atomicAdd(&A.counters->hit, (unsigned long long)s_cnt[2]);
+    }
+  }
+}
+
+// Exclusive scan of the tile counts (one workgroup; <= MAX_KEYS * ntiles entries).
+__global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ tile_counts, int* __restrict__ tile_off,
+                                               int* counts, int depth, int ntiles_alloc, int nkeys) {
+  const int n = counts[depth];
+  const int ntiles = (n + TILE - 1) / TILE;
+  const int total_entries = nkeys * ntiles;
+  __shared__ int s_wave[16];
+  __shared__ int s_carry;
+  if (threadIdx.x == 0) s_carry = 0;
+  __syncthreads();
+  for (int base = 0; base < total_entries; base += 1024) {
+    const int e = base + threadIdx.x;
+    int v = 0;
+    int k = 0, t = 0;
+    if (e < total_entries) {
+      k = e / ntiles;
+      t = e - k * ntiles;
+      v = tile_counts[k * ntiles_alloc + t];
+    }
+    // inclusive wave scan
+    int x = v;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int off = 1; off < 64; off <<= 1) {
+      int y = __shfl_up(x, off);
+      if (lane >= off) x += y;
+    }
+    if (lane == 63) s_wave[wid] = x;
+    __syncthreads();
+    if (wid == 0) {
+      int w = lane < 16 ? s_wave[lane] : 0;
+      for (int off = 1; off < 16; off <<= 1) {
+        int y = __shfl_up(w, off);
+        if (lane >= off) w += y;
+      }
+      if (lane < 16) s_wave[lane] = w;
+    }
+    __syncthreads();
+    const int carry = s_carry;
+    const int excl = carry + (wid > 0 ? s_wave[wid - 1] : 0) + x - v;
+    if (e < total_entries) tile_off[k * ntiles_alloc + t] = excl;
+    __syncthreads();
+    if (threadIdx.x == 1023) s_carry = excl + v;
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) counts[depth + 1] = s_carry;
+}
+
+// Stable compaction (and, on iter 2, the stable sort by materialIdHit).
+template <bool SORT>
+__global__ __launch_bounds__(TILE) void k_scatter(PathBuf src, PathBuf dst, const int* __restrict__ tile_off,
+                                                  const int* counts, int depth, int ntiles_alloc, int compact) {
+  const int n = counts[depth];
+  const int tile = blockIdx.x;
+  if (tile * TILE >= n) return;
+  const int i = tile * TILE + threadIdx.x;
+  const bool valid = i < n;
+  float4 q0, q1, q2;
+  int pm = 0;
+  bool alive = false;
+  if (valid) {
+    q0 = src.p0[i];
+    q1 = src.p1[i];
+    q2 = src.p2[i];
+    pm = src.pm[i];
+    alive = compact ? (fbits(q2.w) != 0) : true;
+  }
+  int dst_i;
+  if (!SORT) {
+    __shared__ int s_wave[TILE / 64];
+    const unsigned long long m = __ballot(alive);
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    if (lane == 0) s_wave[wid] = __popcll(m);
+    __syncthreads();
+    int before = 0;
+    for (int w = 0; w < wid; w++) before += s_wave[w];
+    dst_i = tile_off[tile] + before + (int)lane_prefix(m);
+  } else {
+    __shared__ int s_key[TILE];
+    s_key[threadIdx.x] = alive ? pm : -0x7fffffff;
+    __syncthreads();
+    int r = 0;
+    for (int j = 0; j < (int)threadIdx.x; j++) r += (s_key[j] == pm);
+    dst_i = tile_off[pm * ntiles_alloc + tile] + r;
+  }
+  if (alive) {
+    dst.p0[dst_i] = q0;
+    dst.p1[dst_i] = q1;
+    dst.p2[dst_i] = q2;
+    dst.pm[dst_i] = pm;
+  }
+}
+
+// finalGather (src/pathtrace.cu:2373-2383), including index = paths[index].pixelIndex
+__global__ void k_final_gather(PathBuf paths, const int* counts, int depth, float* image) {
+  const int n = counts[depth];
+  const int index = blockIdx.x * blockDim.x + threadIdx.x;
+  if (index >= n) return;
+  const int j = fbits(paths.p1[index].w) & 0x7fffffff;
+  const float4 c = paths.p2[j];
+  const int pix = fbits(paths.p1[j].w) & 0x7fffffff;
+  image[3 * (size_t)pix + 0] += c.x;
+  image[3 * (size_t)pix + 1] += c.y;
+  image[3 * (size_t)pix + 2] += c.z;
+}
+
+// sendImageToPBO (src/pathtrace.cu:69-89)
+__global__ void k_pbo(const float* image, int npix, int iter, uchar4* pbo) {
+  const int index = blockIdx.x * blockDim.x + threadIdx.x;
+  if (index >= npix) return;
+  int c[3];
+  for (int k = 0; k < 3; k++) {
+    int v = (int)((double)(image[3 * (size_t)index + k] / iter) * 255.0);
+    c[k] = v < 0 ? 0 : (v > 255 ? 255 : v);
+  }
+  pbo[index] = make_uchar4((unsigned char)c[0], (unsigned char)c[1], (unsigned char)c[2], 0);
+}
+
+// debug: unpack the live path array into the reference PathSegment layout
+__global__ void k_unpack(PathBuf src, const int* counts, int depth, kdpt_path_segment* out) {
+  const int n = counts[depth];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 q0 = src.p0[i], q1 = src.p1[i], q2 = src.p2[i];
+  kdpt_path_segment s;
+  s.origin[0] = q0.x; s.origin[1] = q0.y; s.origin[2] = q0.z;
+  s.direction[0] = q1.x; s.direction[1] = q1.y; s.direction[2] = q1.z;
+  const int pw = fbits(q1.w);
+  s.isinside = (uint8_t)((pw >> 31) & 1);
+  s.pad_[0] = s.pad_[1] = s.pad_[2] = 0;
+  s.sdepth = q0.w;
+  s.color[0] = q2.x; s.color[1] = q2.y; s.color[2] = q2.z;
+  s.pixelIndex = pw & 0x7fffffff;
+  s.remainingBounces = fbits(q2.w);
+  s.materialIdHit = src.pm[i];
+  out[i] = s;
+}
+
+__global__ void k_selftest_math(const float* x, int n, float* so, float* co) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n) { so[i] = kdpt_sinf(x[i]); co[i] = kdpt_cosf(x[i]); }
+}
+__global__ void k_selftest_rng(const int* iid, int n, int k, float* u) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Rng r = seeded_rng(iid[3 * i], iid[3 * i + 1], iid[3 * i + 2]);
+  float v = 0;
+  for (int j = 0; j <= k; j++) v = u01(r);
+  u[i] = v;
+}
+__global__ void k_selftest_fresnel(const float* c, int n, float R0, float* f) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  // getFresnelVal with dot(N,-I) == c[i]: F = R0 + (1-R0) * pow(1 - c, 5)
+  double F = (double)R0 + (double)(1.0f - R0) * pow5((double)(1.0f - c[i]));
+  f[i] = (float)F;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------
+// Context
+// ---------------------------------------------------------------------------
+struct kdpt_ctx {
+  int device = 0;
+  hipStream_t stream = nullptr;
+  kdpt_options opt{};
+  kdpt_camera cam{};
+  int traceDepth = 0;
+  int W = 0, H = 0, npix = 0, ntiles = 0, nkeys = 1;
+  int cap = 8;
+  DevScene S{};
+  // owned device memory
+  std::vector<void*> allocs;
+  PathBuf buf[2]{};
+  int cur = 0;
+  float* image = nullptr;
+  bool image_external = false;
+  int* counts = nullptr;  // [cap + 2]
+  int* tile_counts = nullptr;
+  int* tile_off = nullptr;
+  Counters* counters = nullptr;
+  int* h_counts = nullptr;  // pinned
+  hipEvent_t ev0 = nullptr, ev1 = nullptr;
+  std::vector<hipEvent_t> bounce_ev;
+  kdpt_stats stats{};
+  bool count_mode = false;
+};
+
+namespace {
+
+template <typename T>
+int dalloc(kdpt_ctx* c, T** p, size_t n) {
+  void* q = nullptr;
+  HIP_TRY(hipMalloc(&q, std::max<size_t>(n, 1) * sizeof(T)));
+  c->allocs.push_back(q);
+  *p = (T*)q;
+  return KDPT_OK;
+}
+
+template <typename T>
+int dupload(kdpt_ctx* c, T** p, const T* src, size_t n) {
+  int rc = dalloc(c, p, n);
+  if (rc) return rc;
+  if (n) HIP_TRY(hipMemcpy(*p, src, n * sizeof(T), hipMemcpyHostToDevice));
+  return KDPT_OK;
+}
+
+int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count);
+
+}  // namespace
+
+extern "C" {
+
+void kdpt_default_options(kdpt_options* o) {
+  memset(o, 0, sizeof *o);
+  o->focal_length = 6.0f;
+  o->dof_angle = 0.0f;
+  o->softness = 0.0f;
+  o->cacherays = 0;
+  o->antialias = 1;
+  o->enable_sss = 0;
+  o->testing_mode = 0;
+  o->compaction = 1;
+  o->enable_kd = 1;
+  o->viz_kd = 0;
+  o->use_bbox = 0;
+  o->short_stack = 1;
+  o->bounce_cap = 8;
+  o->block_size = 0;
+  o->external_image = nullptr;
+}
+
+const char* kdpt_last_error(void) { return g_last_error.c_str(); }
+
+int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_ctx** out) {
+  if (!sc || !out) return fail(KDPT_ERR_ARG, "null scene/out");
+  *out = nullptr;
+  kdpt_options o;
+  if (opt) o = *opt; else kdpt_default_options(&o);
+  if (!o.enable_kd && sc->has_obj)
+    return fail(KDPT_ERR_UNSUPPORTED, "enable_kd=0 (brute-force pathTraceOneBounce) is not built");
+  if (o.viz_kd) return fail(KDPT_ERR_UNSUPPORTED, "viz_kd (pathTraceOneBounceKDbareBoxes) is not built");
+  if (o.bounce_cap <= 0) o.bounce_cap = 8;
+  if (o.bounce_cap > 30) return fail(KDPT_ERR_ARG, "bounce_cap > 30");
+  if (o.block_size && o.block_size != TILE) return fail(KDPT_ERR_UNSUPPORTED, "block_size must be 0 or 256");
+  const int W = sc->camera.resolution[0], H = sc->camera.resolution[1];
+  if (W <= 0 || H <= 0 || (long long)W * H > (1ll << 30)) return fail(KDPT_ERR_ARG, "bad resolution");
+  if (sc->num_materials > MAX_KEYS) return fail(KDPT_ERR_UNSUPPORTED, "more than 64 materials");
+  // The compact visited-state traversal needs the reference builder's shape:
+  // nodes[i].ID == i, root == node 0, node 1 == root's left child, <= 15 levels.
+  std::vector<int> level;
+  if (sc->has_obj && sc->num_nodes > 0) {
+    const kdpt_node_bare* N = sc->nodes;
+    int root = -1;
+    for (int i = 0; i < sc->num_nodes; i++)
+      if (N[i].parentID == -1) { root = N[i].ID; break; }
+    if (root != 0) return fail(KDPT_ERR_UNSUPPORTED, "root must be node 0");
+    for (int i = 0; i < sc->num_nodes; i++) {
+      if (N[i].ID != i) return fail(KDPT_ERR_UNSUPPORTED, "nodes must be stored in ID order");
+      for (int ch : {N[i].leftID, N[i].rightID})
+        if (ch != -1 && (ch <= i || ch >= sc->num_nodes || N[ch].parentID != i))
+          return fail(KDPT_ERR_ARG, "inconsistent KD node links");
+      if (N[i].triIdSize > 0 && (N[i].triIdStart < 0 || N[i].triIdStart + N[i].triIdSize > sc->num_tris))
+        return fail(KDPT_ERR_ARG, "triangle range out of bounds");
+    }
+    if (sc->num_nodes > 1 && N[0].leftID != 1) return fail(KDPT_ERR_UNSUPPORTED, "node 1 must be root's left child");
+    level.assign(sc->num_nodes, 0);
+    for (int i = 1; i < sc->num_nodes; i++) {
+      level[i] = level[N[i].parentID] + 1;
+      if (level[i] > 15) return fail(KDPT_ERR_UNSUPPORTED, "KD tree deeper than 15 levels");
+    }
+    for (int i = 0; i < sc->num_tris; i++) {
+      int m = sc->tris[i].mtlIdx;
+      if (m < 0 || m >= sc->num_shapes) return fail(KDPT_ERR_ARG, "triangle mtlIdx out of range");
+    }
+  }
+  kdpt_ctx* c = new kdpt_ctx();
+  c->device = device;
+  c->opt = o;
+  c->cam = sc->camera;
+  c->traceDepth = sc->traceDepth;
+  c->W = W;
+  c->H = H;
+  c->npix = W * H;
+  c->ntiles = (c->npix + TILE - 1) / TILE;
+  c->cap = o.bounce_cap;
+  c->nkeys = std::max(1, sc->num_materials);
+  auto bail = [&](int rc) {
+    kdpt_destroy(c);
+    return rc;
+  };
+  if (hipSetDevice(device) != hipSuccess) return bail(fail(KDPT_ERR_HIP, "hipSetDevice failed"));
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
+    return bail(fail(KDPT_ERR_HIP, "hipStreamCreate failed"));
+  int rc;
+  // geoms / materials
+  std::vector<DevGeom> dg(sc->num_geoms);
+  for (int i = 0; i < sc->num_geoms; i++) {
+    dg[i].type = sc->geoms[i].type;
+    dg[i].materialid = sc->geoms[i].materialid;
+    memcpy(dg[i].transform, sc->geoms[i].transform, 64);
+    memcpy(dg[i].inverseTransform, sc->geoms[i].inverseTransform, 64);
+    memcpy(dg[i].invTranspose, sc->geoms[i].invTranspose, 64);
+    if (dg[i].materialid < 0 || dg[i].materialid >= sc->num_materials)
+      return bail(fail(KDPT_ERR_ARG, "geom materialid out of range"));
+  }
+  std::vector<DevMaterial> dm(sc->num_materials);
+  for (int i = 0; i < sc->num_materials; i++) {
+    const kdpt_material& m = sc->materials[i];
+    DevMaterial& d = dm[i];
+    memcpy(d.color, m.color, 12);
+    d.spec_exponent = m.specular_exponent;
+    memcpy(d.spec_color, m.specular_color, 12);
+    d.hasReflective = m.hasReflective;
+    d.hasRefractive = m.hasRefractive;
+    d.indexOfRefraction = m.indexOfRefraction;
+    d.emittance = m.emittance;
+    memcpy(d.transmittance, m.transmittance, 12);
+    // glm::pow((1.0f - ior) / (1.0f + ior), 2.0f): powf(x, 2) folds to x * x
+    float rr = (1.0f - m.indexOfRefraction) / (1.0f + m.indexOfRefraction);
+    d.fresnel_R0 = rr * rr;
+    d.pad_[0] = d.pad_[1] = d.pad_[2] = 0;
+  }
+  DevGeom* d_geoms;
+  DevMaterial* d_mats;
+  if ((rc = dupload(c, &d_geoms, dg.data(), dg.size()))) return bail(rc);
+  if ((rc = dupload(c, &d_mats, dm.data(), dm.size()))) return bail(rc);
+  c->S.geoms = d_geoms;
+  c->S.num_geoms = sc->num_geoms;
+  c->S.materials = d_mats;
+  c->S.num_materials = sc->num_materials;
+  c->S.has_obj = sc->has_obj ? 1 : 0;
+  c->S.num_nodes = sc->has_obj ? sc->num_nodes : 0;
+  c->S.root = 0;
+  c->S.n0_left = c->S.n0_right = c->S.n1_left = c->S.n1_right = -1;
+  if (sc->has_obj && sc->num_nodes > 0) {
+    const int nn = sc->num_nodes, nt = sc->num_tris;
+    std::vector<float4> b0(nn), b1(nn), tv(nt), e1(nt), e2(nt), n0(nt), n1(nt), n2(nt);
+    std::vector<int4> meta(nn);
+    for (int i = 0; i < nn; i++) {
+      const kdpt_node_bare& N = sc->nodes[i];
+      b0[i] = make_float4(N.mins[0], N.mins[1], N.mins[2], N.maxs[0]);
+      b1[i] = make_float4(N.maxs[1], N.maxs[2], ibits(N.leftID), ibits(N.rightID));
+      meta[i] = make_int4(N.parentID, N.triIdStart, N.triIdSize, N.axis);
+    }
+    for (int i = 0; i < nt; i++) {
+      const kdpt_tri_bare& T = sc->tris[i];
+      // glm::intersectRayTriangle's e1 = v1 - v0, e2 = v2 - v0 in float: same bits here
+      tv[i] = make_float4(T.x1, T.y1, T.z1, ibits(T.mtlIdx));
+      e1[i] = make_float4(T.x2 - T.x1, T.y2 - T.y1, T.z2 - T.z1, 0.0f);
+      e2[i] = make_float4(T.x3 - T.x1, T.y3 - T.y1, T.z3 - T.z1, 0.0f);
+      n0[i] = make_float4(T.nx1, T.ny1, T.nz1, 0.0f);
+      n1[i] = make_float4(T.nx2, T.ny2, T.nz2, 0.0f);
+      n2[i] = make_float4(T.nx3, T.ny3, T.nz3, 0.0f);
+    }
+    float4 *db0, *db1, *dtv, *de1, *de2, *dn0, *dn1, *dn2;
+    int4* dmeta;
+    int* doff;
+    if ((rc = dupload(c, &db0, b0.data(), nn)) || (rc = dupload(c, &db1, b1.data(), nn)) ||
+        (rc = dupload(c, &dmeta, meta.data(), nn)) || (rc = dupload(c, &dtv, tv.data(), nt)) ||
+        (rc = dupload(c, &de1, e1.data(), nt)) || (rc = dupload(c, &de2, e2.data(), nt)) ||
+        (rc = dupload(c, &dn0, n0.data(), nt)) || (rc = dupload(c, &dn1, n1.data(), nt)) ||
+        (rc = dupload(c, &dn2, n2.data(), nt)) ||
+        (rc = dupload(c, &doff, sc->obj_materialOffsets, (size_t)sc->num_shapes)))
+      return bail(rc);
+    c->S.nbox0 = db0;
+    c->S.nbox1 = db1;
+    c->S.nmeta = dmeta;
+    c->S.tv0 = dtv;
+    c->S.te1 = de1;
+    c->S.te2 = de2;
+    c->S.tn0 = dn0;
+    c->S.tn1 = dn1;
+    c->S.tn2 = dn2;
+    c->S.obj_material_offsets = doff;
+    c->S.n0_left = sc->nodes[0].leftID;
+    c->S.n0_right = sc->nodes[0].rightID;
+    if (nn > 1) {
+      c->S.n1_left = sc->nodes[1].leftID;
+      c->S.n1_right = sc->nodes[1].rightID;
+    }
+  } else {
+    c->S.has_obj = 0;
+  }
+  for (int b = 0; b < 2; b++) {
+    if ((rc = dalloc(c, &c->buf[b].p0, c->npix)) || (rc = dalloc(c, &c->buf[b].p1, c->npix)) ||
+        (rc = dalloc(c, &c->buf[b].p2, c->npix)) || (rc = dalloc(c, &c->buf[b].pm, c->npix)))
+      return bail(rc);
+    if (hipMemset(c->buf[b].pm, 0, sizeof(int) * c->npix) != hipSuccess) return bail(fail(KDPT_ERR_HIP, "memset"));
+  }
+  if (o.external_image) {
+    c->image = o.external_image;
+    c->image_external = true;
+  } else if ((rc = dalloc(c, &c->image, 3 * (size_t)c->npix))) {
+    return bail(rc);
+  }
+  if ((rc = dalloc(c, &c->counts, c->cap + 2)) || (rc = dalloc(c, &c->tile_counts, (size_t)MAX_KEYS * c->ntiles)) ||
+      (rc = dalloc(c, &c->tile_off, (size_t)MAX_KEYS * c->ntiles)) || (rc = dalloc(c, &c->counters, 1)))
+    return bail(rc);
+  if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 2), hipHostMallocDefault) != hipSuccess)
+    return bail(fail(KDPT_ERR_HIP, "hipHostMalloc"));
+  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
+    return bail(fail(KDPT_ERR_HIP, "hipEventCreate"));
+  c->bounce_ev.resize(2 * (size_t)c->cap);
+  for (auto& e : c->bounce_ev)
+    if (hipEventCreate(&e) != hipSuccess) return bail(fail(KDPT_ERR_HIP, "hipEventCreate"));
+  if ((rc = kdpt_reset(c))) return bail(rc);
+  *out = c;
+  return KDPT_OK;
+}
+
+int kdpt_reset(kdpt_ctx* c) {
+  if (!c) return fail(KDPT_ERR_ARG, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemsetAsync(c->image, 0, sizeof(float) * 3 * (size_t)c->npix, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  memset(&c->stats, 0, sizeof c->stats);
+  return KDPT_OK;
+}
+
+int kdpt_trace_iteration_async(kdpt_ctx* c, int frame, int iter) {
+  (void)frame;  // unused by the reference too
+  if (!c) return fail(KDPT_ERR_ARG, "null ctx");
+  return launch_iteration(c, iter, -1, false);
+}
+
+int kdpt_synchronize(kdpt_ctx* c) {
+  if (!c) return fail(KDPT_ERR_ARG, "null ctx");
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return KDPT_OK;
+}
+
+int kdpt_trace_iteration(kdpt_ctx* c, int frame, int iter) {
+  (void)frame;
+  if (!c) return fail(KDPT_ERR_ARG, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipEventRecord(c->ev0, c->stream));
+  int rc = launch_iteration(c, iter, -1, c->count_mode);
+  if (rc) return rc;
+  HIP_TRY(hipEventRecord(c->ev1, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts, sizeof(int) * (c->cap + 1), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  float ms = 0;
+  HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
+  c->stats.ms_last_iteration = ms;
+  c->stats.iterations++;
+  long long seg = 0;
+  int bounces = 0;
+  for (int d = 0; d < 32; d++) c->stats.seg_per_bounce[d] = 0;
+  for (int d = 0; d < c->cap; d++) {
+    const int nd = c->h_counts[d];
+    if (d > 0 && c->h_counts[d] <= 0) break;  // the reference stops once num_paths <= 0
+    seg += nd;
+    if (d < 32) c->stats.seg_per_bounce[d] = nd;
+    bounces = d + 1;
+    if (c->opt.compaction && c->h_counts[d + 1] <= 0) break;
+  }
+  c->stats.segments = seg;
+  c->stats.bounces = bounces;
+  c->stats.total_segments += seg;
+  if (c->opt.testing_mode) {
+    float tot = 0;
+    for (int d = 0; d < bounces; d++) {
+      float b = 0;
+      if (hipEventElapsedTime(&b, c->bounce_ev[2 * d], c->bounce_ev[2 * d + 1]) == hipSuccess) tot += b;
+    }
+    c->stats.ms_intersect = tot;
+  }
+  return KDPT_OK;
+}
+
+int kdpt_read_image(kdpt_ctx* c, float* rgb) {
+  if (!c || !rgb) return fail(KDPT_ERR_ARG, "null arg");
+  HIP_TRY(hipSetDevice(c->device));
+  HIP_TRY(hipMemcpyAsync(rgb, c->image, sizeof(float) * 3 * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return KDPT_OK;
+}
+
+int kdpt_write_pbo(kdpt_ctx* c, int iter, uint8_t* rgba) {
+  if (!c || !rgba || iter == 0) return fail(KDPT_ERR_ARG, "bad arg");
+  HIP_TRY(hipSetDevice(c->device));
+  uchar4* d = nullptr;
+  HIP_TRY(hipMalloc((void**)&d, sizeof(uchar4) * (size_t)c->npix));
+  hipLaunchKernelGGL(k_pbo, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->image, c->npix, iter, d);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(rgba, d, sizeof(uchar4) * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  HIP_TRY(hipFree(d));
+  return KDPT_OK;
+}
+
+int kdpt_get_stats(kdpt_ctx* c, kdpt_stats* st) {
+  if (!c || !st) return fail(KDPT_ERR_ARG, "null arg");
+  *st = c->stats;
+  return KDPT_OK;
+}
+
+int kdpt_image_device_ptr(kdpt_ctx* c, void** p) {
+  if (!c || !p) return fail(KDPT_ERR_ARG, "null arg");
+  *p = c->image;
+  return KDPT_OK;
+}
+
+int kdpt_destroy(kdpt_ctx* c) {
+  if (!c) return KDPT_OK;
+  hipSetDevice(c->device);
+  if (c->stream) hipStreamSynchronize(c->stream);
+  for (void* p : c->allocs) hipFree(p);
+  if (c->h_counts) hipHostFree(c->h_counts);
+  if (c->ev0) hipEventDestroy(c->ev0);
+  if (c->ev1) hipEventDestroy(c->ev1);
+  for (auto e : c->bounce_ev)
+    if (e) hipEventDestroy(e);
+  if (c->stream) hipStreamDestroy(c->stream);
+  delete c;
+  return KDPT_OK;
+}
+
+int kdpt_debug_paths(kdpt_ctx* c, int iter, int stop_depth, kdpt_path_segment* out, int* npaths) {
+  if (!c || !out || stop_depth < 0 || stop_depth >= c->cap) return fail(KDPT_ERR_ARG, "bad arg");
+  HIP_TRY(hipSetDevice(c->device));
+  // run on a scratch image so the accumulation buffer is untouched
+  float* saved = c->image;
+  float* scratch = nullptr;
+  HIP_TRY(hipMalloc((void**)&scratch, sizeof(float) * 3 * (size_t)c->npix));
+  HIP_TRY(hipMemset(scratch, 0, sizeof(float) * 3 * (size_t)c->npix));
+  c->image = scratch;
+  int rc = launch_iteration(c, iter, stop_depth, false);
+  c->image = saved;
+  if (rc) { hipFree(scratch); return rc; }
+  kdpt_path_segment* d = nullptr;
+  HIP_TRY(hipMalloc((void**)&d, sizeof(kdpt_path_segment) * (size_t)c->npix));
+  const int depth_slot = stop_depth + 1;
+  hipLaunchKernelGGL(k_unpack, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->buf[c->cur], c->counts,
+                     depth_slot, d);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts, sizeof(int) * (c->cap + 2), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  const int n = c->h_counts[depth_slot];
+  *npaths = n;
+  HIP_TRY(hipMemcpy(out, d, sizeof(kdpt_path_segment) * (size_t)n, hipMemcpyDeviceToHost));
+  hipFree(d);
+  hipFree(scratch);
+  return KDPT_OK;
+}
+
+// Roofline counters: one extra (untimed) iteration with per-path AABB/triangle/hit counts.
+int kdpt_count_iteration(kdpt_ctx* c, int iter, unsigned long long* aabb_tri_hit) {
+  if (!c || !aabb_tri_hit) return fail(KDPT_ERR_ARG, "null arg");
+  HIP_TRY(hipSetDevice(c->device));
+  float* saved = c->image;
+  float* scratch = nullptr;
+  HIP_TRY(hipMalloc((void**)&scratch, sizeof(float) * 3 * (size_t)c->npix));
+  HIP_TRY(hipMemset(scratch, 0, sizeof(float) * 3 * (size_t)c->npix));
+  HIP_TRY(hipMemset(c->counters, 0, sizeof(Counters)));
+  c->image = scratch;
+  int rc = launch_iteration(c, iter, -1, true);
+  c->image = saved;
+  Counters h{};
+  if (!rc) {
+    HIP_TRY(hipMemcpyAsync(&h, c->counters, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  hipFree(scratch);
+  aabb_tri_hit[0] = h.aabb;
+  aabb_tri_hit[1] = h.tri;
+  aabb_tri_hit[2] = h.hit;
+  return rc;
+}
+
+int kdpt_selftest_math(const float* x, int n, float* so, float* co) {
+  float *dx, *ds, *dc;
+  HIP_TRY(hipMalloc((void**)&dx, sizeof(float) * n));
+  HIP_TRY(hipMalloc((void**)&ds, sizeof(float) * n));
+  HIP_TRY(hipMalloc((void**)&dc, sizeof(float) * n));
+  HIP_TRY(hipMemcpy(dx, x, sizeof(float) * n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_selftest_math, dim3((n + 255) / 256), dim3(256), 0, 0, dx, n, ds, dc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(so, ds, sizeof(float) * n, hipMemcpyDeviceToHost));
+  HIP_TRY(hipMemcpy(co, dc, sizeof(float) * n, hipMemcpyDeviceToHost));
+  hipFree(dx); hipFree(ds); hipFree(dc);
+  return KDPT_OK;
+}
+
+int kdpt_selftest_rng(const int* iid, int n, int k, float* u) {
+  int* di;
+  float* du;
+  HIP_TRY(hipMalloc((void**)&di, sizeof(int) * 3 * n));
+  HIP_TRY(hipMalloc((void**)&du, sizeof(float) * n));
+  HIP_TRY(hipMemcpy(di, iid, sizeof(int) * 3 * n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_selftest_rng, dim3((n + 255) / 256), dim3(256), 0, 0, di, n, k, du);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(u, du, sizeof(float) * n, hipMemcpyDeviceToHost));
+  hipFree(di); hipFree(du);
+  return KDPT_OK;
+}
+
+int kdpt_selftest_fresnel(const float* cs, int n, float ior, float* f) {
+  float *dc, *df;
+  HIP_TRY(hipMalloc((void**)&dc, sizeof(float) * n));
+  HIP_TRY(hipMalloc((void**)&df, sizeof(float) * n));
+  HIP_TRY(hipMemcpy(dc, cs, sizeof(float) * n, hipMemcpyHostToDevice));
+  float rr = (1.0f - ior) / (1.0f + ior);
+  hipLaunchKernelGGL(k_selftest_fresnel, dim3((n + 255) / 256), dim3(256), 0, 0, dc, n, rr * rr, df);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(f, df, sizeof(float) * n, hipMemcpyDeviceToHost));
+  hipFree(dc); hipFree(df);
+  return KDPT_OK;
+}
+
+}  // extern "C"
+
+namespace {
+
+template <bool HYBRID, bool COMPACT, bool SORT>
+void launch_bounce(kdpt_ctx* c, const BounceArgs& a, bool count) {
+  if (count)
+    hipLaunchKernelGGL((k_bounce<HYBRID, COMPACT, SORT, true>), dim3(c->ntiles), dim3(TILE), 0, c->stream, a);
+  else
+    hipLaunchKernelGGL((k_bounce<HYBRID, COMPACT, SORT, false>), dim3(c->ntiles), dim3(TILE), 0, c->stream, a);
+}
+
+int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
+  const int gen_iter = c->opt.cacherays ? 1 : iter;
+  c->cur = 0;
+  hipLaunchKernelGGL(k_gen_rays, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->cam, gen_iter,
+                     c->traceDepth, c->buf[0], c->opt.focal_length, c->opt.dof_angle, c->opt.antialias, c->counts,
+                     c->cap + 2);
+  HIP_TRY(hipGetLastError());
+  const bool compact = c->opt.compaction != 0;
+  const bool sort = (iter == 2);
+  for (int depth = 0; depth < c->cap; depth++) {
+    BounceArgs a;
+    a.S = c->S;
+    a.paths = c->buf[c->cur];
+    a.image = c->image;
+    a.counts = c->counts;
+    a.depth = depth;
+    a.iter = iter;
+    a.softness = c->opt.softness;
+    a.enable_sss = c->opt.enable_sss;
+    a.tile_counts = c->tile_counts;
+    a.ntiles = c->ntiles;
+    a.nkeys = c->nkeys;
+    a.counters = c->counters;
+    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(c->bounce_ev[2 * depth], c->stream));
+    const bool hyb = c->opt.short_stack != 0;
+    if (hyb) {
+      if (compact) { if (sort) launch_bounce<true, true, true>(c, a, count); else launch_bounce<true, true, false>(c, a, count); }
+      else { if (sort) launch_bounce<true, false, true>(c, a, count); else launch_bounce<true, false, false>(c, a, count); }
+    } else {
+      if (compact) { if (sort) launch_bounce<false, true, true>(c, a, count); else launch_bounce<false, true, false>(c, a, count); }
+      else { if (sort) launch_bounce<false, false, true>(c, a, count); else launch_bounce<false, false, false>(c, a, count); }
+    }
+    HIP_TRY(hipGetLastError());
+    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(c->bounce_ev[2 * depth + 1], c->stream));
+    if (compact || sort) {
+      hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, c->stream, c->tile_counts, c->tile_off, c->counts, depth,
+                         c->ntiles, sort ? c->nkeys : 1);
+      HIP_TRY(hipGetLastError());
+      const int nxt = c->cur ^ 1;
+      if (sort)
+        hipLaunchKernelGGL(k_scatter<true>, dim3(c->ntiles), dim3(TILE), 0, c->stream, c->buf[c->cur], c->buf[nxt],
+                           c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0);
+      else
+        hipLaunchKernelGGL(k_scatter<false>, dim3(c->ntiles), dim3(TILE), 0, c->stream, c->buf[c->cur], c->buf[nxt],
+                           c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0);
+      HIP_TRY(hipGetLastError());
+      c->cur = nxt;
+    } else {
+      // no compaction, no sort: the live range stays the whole image
+      HIP_TRY(hipMemcpyAsync(c->counts + depth + 1, c->counts + depth, sizeof(int), hipMemcpyDeviceToDevice,
+                             c->stream));
+    }
+    if (stop_depth == depth) return KDPT_OK;
+  }
+  if (!compact) {
+    hipLaunchKernelGGL(k_final_gather, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->buf[c->cur],
+                       c->counts, c->cap, c->image);
+    HIP_TRY(hipGetLastError());
+  }
+  return KDPT_OK;
+}
+
+}  // namespace

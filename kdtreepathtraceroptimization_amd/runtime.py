@@ -1,0 +1,387 @@
+"""ctypes binding of the C-ABI in include/kdpt.h.
+
+Python here is plumbing (tests, bench, torch.distributed); the path tracer is
+the in-tree HIP library ``libkdpt.so``.  There is no CPU fallback: if the
+library is missing or cannot open a HIP device every entry point raises.
+
+Mirrors the reference's operator interface (src/pathtrace.h:6-21):
+``PathTracer(scene, options)``          ~ pathtraceInit(Scene*, enablekd)
+``PathTracer.trace_iteration(iter)``    ~ pathtrace(pbo, frame, iter, ...flags)
+``PathTracer.close()``                  ~ pathtraceFree(Scene*, enablekd)
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from dataclasses import dataclass
+from typing import Optional
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "libkdpt.so")
+
+KDPT_OK = 0
+
+
+class KdptError(RuntimeError):
+    pass
+
+
+# ---------------------------------------------------------------- structs
+class Geom(C.Structure):  # struct Geom, src/sceneStructs.h:22-31
+    _fields_ = [("type", C.c_int), ("materialid", C.c_int), ("translation", C.c_float * 3),
+                ("rotation", C.c_float * 3), ("scale", C.c_float * 3), ("transform", C.c_float * 16),
+                ("inverseTransform", C.c_float * 16), ("invTranspose", C.c_float * 16)]
+
+
+class Material(C.Structure):  # struct Material, src/sceneStructs.h:33-44
+    _fields_ = [("color", C.c_float * 3), ("specular_exponent", C.c_float), ("specular_color", C.c_float * 3),
+                ("hasReflective", C.c_float), ("hasRefractive", C.c_float), ("indexOfRefraction", C.c_float),
+                ("emittance", C.c_float), ("transmittance", C.c_float * 3)]
+
+
+class Camera(C.Structure):  # struct Camera, src/sceneStructs.h:46-55
+    _fields_ = [("resolution", C.c_int * 2), ("position", C.c_float * 3), ("lookAt", C.c_float * 3),
+                ("view", C.c_float * 3), ("up", C.c_float * 3), ("right", C.c_float * 3), ("fov", C.c_float * 2),
+                ("pixelLength", C.c_float * 2)]
+
+
+class NodeBare(C.Structure):  # KDN::NodeBare, src/KDnode.h:64-82
+    _fields_ = [("axis", C.c_int), ("splitPos", C.c_float), ("mins", C.c_float * 3), ("maxs", C.c_float * 3),
+                ("ID", C.c_int), ("parentID", C.c_int), ("leftID", C.c_int), ("rightID", C.c_int),
+                ("triIdStart", C.c_int), ("triIdSize", C.c_int), ("tmin", C.c_float), ("tmax", C.c_float)]
+
+
+class TriBare(C.Structure):  # KDN::TriBare, src/KDnode.h:51-62
+    _fields_ = [(n, C.c_float) for n in ("x1", "x2", "x3", "y1", "y2", "y3", "z1", "z2", "z3",
+                                          "nx1", "nx2", "nx3", "ny1", "ny2", "ny3", "nz1", "nz2", "nz3")] + [
+        ("mtlIdx", C.c_int)]
+
+
+class PathSegment(C.Structure):  # struct PathSegment, src/sceneStructs.h:65-71
+    _fields_ = [("origin", C.c_float * 3), ("direction", C.c_float * 3), ("isinside", C.c_uint8),
+                ("pad_", C.c_uint8 * 3), ("sdepth", C.c_float), ("color", C.c_float * 3), ("pixelIndex", C.c_int),
+                ("remainingBounces", C.c_int), ("materialIdHit", C.c_int)]
+
+
+class Scene(C.Structure):
+    _fields_ = [("camera", Camera), ("traceDepth", C.c_int), ("geoms", C.POINTER(Geom)), ("num_geoms", C.c_int),
+                ("materials", C.POINTER(Material)), ("num_materials", C.c_int), ("has_obj", C.c_int),
+                ("nodes", C.POINTER(NodeBare)), ("num_nodes", C.c_int), ("tris", C.POINTER(TriBare)),
+                ("num_tris", C.c_int), ("obj_materialOffsets", C.POINTER(C.c_int)), ("num_shapes", C.c_int)]
+
+
+class Options(C.Structure):
+    _fields_ = [("focal_length", C.c_float), ("dof_angle", C.c_float), ("softness", C.c_float),
+                ("cacherays", C.c_int), ("antialias", C.c_int), ("enable_sss", C.c_int), ("testing_mode", C.c_int),
+                ("compaction", C.c_int), ("enable_kd", C.c_int), ("viz_kd", C.c_int), ("use_bbox", C.c_int),
+                ("short_stack", C.c_int), ("bounce_cap", C.c_int), ("block_size", C.c_int),
+                ("external_image", C.c_void_p)]
+
+
+class Stats(C.Structure):
+    _fields_ = [("segments", C.c_longlong), ("seg_per_bounce", C.c_longlong * 32), ("bounces", C.c_int),
+                ("iterations", C.c_int), ("ms_last_iteration", C.c_float), ("ms_intersect", C.c_float),
+                ("total_segments", C.c_longlong)]
+
+
+class SceneDesc(C.Structure):
+    _fields_ = [("res", C.c_int * 2), ("fovy", C.c_float), ("iterations", C.c_int), ("traceDepth", C.c_int),
+                ("eye", C.c_float * 3), ("lookAt", C.c_float * 3), ("up", C.c_float * 3),
+                ("num_materials", C.c_int), ("materials", C.POINTER(Material)), ("num_geoms", C.c_int),
+                ("geom_type", C.POINTER(C.c_int)), ("geom_material", C.POINTER(C.c_int)),
+                ("geom_trs", C.POINTER(C.c_float)), ("ntri", C.c_int), ("verts9", C.POINTER(C.c_float)),
+                ("norms9", C.POINTER(C.c_float)), ("shape_of_tri", C.POINTER(C.c_int)), ("num_shapes", C.c_int),
+                ("shape_materials", C.POINTER(Material)), ("kd_max_depth", C.c_int)]
+
+
+assert C.sizeof(Geom) == 236 and C.sizeof(Material) == 56 and C.sizeof(Camera) == 84
+assert C.sizeof(NodeBare) == 64 and C.sizeof(TriBare) == 76 and C.sizeof(PathSegment) == 56
+
+EXPORTS = [
+    "kdpt_default_options", "kdpt_create", "kdpt_trace_iteration", "kdpt_trace_iteration_async", "kdpt_synchronize",
+    "kdpt_read_image", "kdpt_write_pbo", "kdpt_reset", "kdpt_get_stats", "kdpt_destroy", "kdpt_last_error",
+    "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_selftest_math", "kdpt_selftest_rng",
+    "kdpt_selftest_fresnel", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
+]
+
+_lib = None
+
+
+def load_library(path: str = LIB_PATH) -> C.CDLL:
+    """Load the in-tree libkdpt.so (HIP runtime shared with torch when torch is imported)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise KdptError(f"{path} is missing: run `python -m kdtreepathtraceroptimization_amd._build` "
+                        "(there is no CPU fallback)")
+    try:  # one HIP runtime per process: let torch's libamdhip64 (same soname) win if present
+        import torch  # noqa: F401
+    except Exception:
+        pass
+    lib = C.CDLL(path)
+    P = C.POINTER
+    lib.kdpt_default_options.argtypes = [P(Options)]
+    lib.kdpt_default_options.restype = None
+    lib.kdpt_create.argtypes = [P(Scene), P(Options), C.c_int, P(C.c_void_p)]
+    lib.kdpt_trace_iteration.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lib.kdpt_trace_iteration_async.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lib.kdpt_synchronize.argtypes = [C.c_void_p]
+    lib.kdpt_read_image.argtypes = [C.c_void_p, P(C.c_float)]
+    lib.kdpt_write_pbo.argtypes = [C.c_void_p, C.c_int, P(C.c_uint8)]
+    lib.kdpt_reset.argtypes = [C.c_void_p]
+    lib.kdpt_get_stats.argtypes = [C.c_void_p, P(Stats)]
+    lib.kdpt_destroy.argtypes = [C.c_void_p]
+    lib.kdpt_last_error.restype = C.c_char_p
+    lib.kdpt_image_device_ptr.argtypes = [C.c_void_p, P(C.c_void_p)]
+    lib.kdpt_debug_paths.argtypes = [C.c_void_p, C.c_int, C.c_int, P(PathSegment), P(C.c_int)]
+    lib.kdpt_count_iteration.argtypes = [C.c_void_p, C.c_int, P(C.c_ulonglong)]
+    lib.kdpt_selftest_math.argtypes = [P(C.c_float), C.c_int, P(C.c_float), P(C.c_float)]
+    lib.kdpt_selftest_rng.argtypes = [P(C.c_int), C.c_int, C.c_int, P(C.c_float)]
+    lib.kdpt_selftest_fresnel.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
+    lib.kdpt_scene_load.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, P(C.c_void_p)]
+    lib.kdpt_scene_build.argtypes = [P(SceneDesc), P(C.c_void_p)]
+    lib.kdpt_scene_view.argtypes = [C.c_void_p, P(Scene)]
+    lib.kdpt_scene_free.argtypes = [C.c_void_p]
+    _lib = lib
+    return lib
+
+
+def _check(rc: int, what: str):
+    if rc != KDPT_OK:
+        msg = load_library().kdpt_last_error().decode(errors="replace")
+        raise KdptError(f"{what} failed ({rc}): {msg}")
+
+
+def _fptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def _iptr(a: np.ndarray):
+    return a.ctypes.data_as(C.POINTER(C.c_int))
+
+
+MATERIAL_DTYPE = np.dtype([("color", "<f4", 3), ("specular_exponent", "<f4"), ("specular_color", "<f4", 3),
+                           ("hasReflective", "<f4"), ("hasRefractive", "<f4"), ("indexOfRefraction", "<f4"),
+                           ("emittance", "<f4"), ("transmittance", "<f4", 3)])
+assert MATERIAL_DTYPE.itemsize == 56
+
+
+@dataclass
+class SceneDescription:
+    """What the reference's parsers produce before any matrix/camera/KD work."""
+    res: tuple
+    fovy: float
+    iterations: int
+    trace_depth: int
+    eye: np.ndarray
+    look_at: np.ndarray
+    up: np.ndarray
+    materials: np.ndarray          # MATERIAL_DTYPE[nm]
+    geom_type: np.ndarray          # int32[ng]
+    geom_material: np.ndarray      # int32[ng]
+    geom_trs: np.ndarray           # float32[ng, 9]
+    verts9: Optional[np.ndarray] = None   # float32[ntri, 9]
+    norms9: Optional[np.ndarray] = None   # float32[ntri, 9]
+    shape_of_tri: Optional[np.ndarray] = None  # int32[ntri]
+    shape_materials: Optional[np.ndarray] = None  # MATERIAL_DTYPE[nshapes]
+
+    def with_overrides(self, res=None, depth=None) -> "SceneDescription":
+        import dataclasses
+        d = dataclasses.replace(self)
+        if res is not None:
+            d.res = (int(res[0]), int(res[1]))
+        if depth is not None:
+            d.trace_depth = int(depth)
+        return d
+
+    def to_c(self):
+        """Build a SceneDesc (the numpy arrays it points into are returned to keep them alive)."""
+        keep = []
+
+        def arr(x, dt):
+            a = np.ascontiguousarray(x, dtype=dt)
+            keep.append(a)
+            return a
+
+        mats = arr(self.materials, MATERIAL_DTYPE)
+        d = SceneDesc()
+        d.res[0], d.res[1] = int(self.res[0]), int(self.res[1])
+        d.fovy = float(np.float32(self.fovy))
+        d.iterations = int(self.iterations)
+        d.traceDepth = int(self.trace_depth)
+        for i in range(3):
+            d.eye[i], d.lookAt[i], d.up[i] = float(self.eye[i]), float(self.look_at[i]), float(self.up[i])
+        d.num_materials = len(mats)
+        d.materials = mats.ctypes.data_as(C.POINTER(Material))
+        gt, gm, gtrs = arr(self.geom_type, np.int32), arr(self.geom_material, np.int32), arr(self.geom_trs, np.float32)
+        d.num_geoms = len(gt)
+        d.geom_type, d.geom_material, d.geom_trs = _iptr(gt), _iptr(gm), _fptr(gtrs)
+        if self.verts9 is not None and len(self.verts9):
+            v9, n9 = arr(self.verts9, np.float32), arr(self.norms9, np.float32)
+            st, sm = arr(self.shape_of_tri, np.int32), arr(self.shape_materials, MATERIAL_DTYPE)
+            d.ntri = len(st)
+            d.verts9, d.norms9, d.shape_of_tri = _fptr(v9), _fptr(n9), _iptr(st)
+            d.num_shapes = len(sm)
+            d.shape_materials = sm.ctypes.data_as(C.POINTER(Material))
+        d.kd_max_depth = 13
+        return d, keep
+
+
+class SceneData:
+    """A built scene (Scene::geoms/materials/newNodesBare/newTrianglesBare + camera), owned by libkdpt."""
+
+    def __init__(self, handle: C.c_void_p):
+        self._h = handle
+        self.view = Scene()
+        _check(load_library().kdpt_scene_view(self._h, C.byref(self.view)), "kdpt_scene_view")
+
+    @classmethod
+    def from_files(cls, scene_path: str, obj_path: Optional[str] = None, res=None, depth=None) -> "SceneData":
+        lib = load_library()
+        h = C.c_void_p()
+        w, hh = (res if res is not None else (0, 0))
+        rc = lib.kdpt_scene_load(scene_path.encode(), obj_path.encode() if obj_path else None, int(w), int(hh),
+                                 int(depth or 0), C.byref(h))
+        _check(rc, f"kdpt_scene_load({scene_path}, {obj_path})")
+        return cls(h)
+
+    @classmethod
+    def from_description(cls, desc: SceneDescription) -> "SceneData":
+        lib = load_library()
+        d, keep = desc.to_c()
+        h = C.c_void_p()
+        _check(lib.kdpt_scene_build(C.byref(d), C.byref(h)), "kdpt_scene_build")
+        del keep
+        return cls(h)
+
+    @property
+    def resolution(self):
+        return int(self.view.camera.resolution[0]), int(self.view.camera.resolution[1])
+
+    def nodes_bytes(self) -> bytes:
+        return C.string_at(self.view.nodes, C.sizeof(NodeBare) * self.view.num_nodes)
+
+    def tris_bytes(self) -> bytes:
+        return C.string_at(self.view.tris, C.sizeof(TriBare) * self.view.num_tris)
+
+    def geoms_bytes(self) -> bytes:
+        return C.string_at(self.view.geoms, C.sizeof(Geom) * self.view.num_geoms)
+
+    def materials_bytes(self) -> bytes:
+        return C.string_at(self.view.materials, C.sizeof(Material) * self.view.num_materials)
+
+    def camera_bytes(self) -> bytes:
+        return bytes(self.view.camera)
+
+    def close(self):
+        if self._h:
+            load_library().kdpt_scene_free(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+def default_options(**overrides) -> Options:
+    o = Options()
+    load_library().kdpt_default_options(C.byref(o))
+    for k, v in overrides.items():
+        if not hasattr(o, k):
+            raise KeyError(k)
+        setattr(o, k, v)
+    return o
+
+
+class PathTracer:
+    """One device context: pathtraceInit / pathtrace / pathtraceFree."""
+
+    def __init__(self, scene: SceneData, options: Optional[Options] = None, device: int = 0):
+        self.scene = scene
+        self.lib = load_library()
+        self.opt = options if options is not None else default_options()
+        self._ctx = C.c_void_p()
+        _check(self.lib.kdpt_create(C.byref(scene.view), C.byref(self.opt), int(device), C.byref(self._ctx)),
+               "kdpt_create")
+        self.width, self.height = scene.resolution
+
+    def trace_iteration(self, iteration: int, frame: int = 0):
+        _check(self.lib.kdpt_trace_iteration(self._ctx, int(frame), int(iteration)), "kdpt_trace_iteration")
+
+    def trace_iteration_async(self, iteration: int, frame: int = 0):
+        _check(self.lib.kdpt_trace_iteration_async(self._ctx, int(frame), int(iteration)), "kdpt_trace_iteration_async")
+
+    def synchronize(self):
+        _check(self.lib.kdpt_synchronize(self._ctx), "kdpt_synchronize")
+
+    def image(self) -> np.ndarray:
+        out = np.empty((self.height, self.width, 3), dtype=np.float32)
+        _check(self.lib.kdpt_read_image(self._ctx, _fptr(out)), "kdpt_read_image")
+        return out
+
+    def pbo(self, iteration: int) -> np.ndarray:
+        out = np.empty((self.height, self.width, 4), dtype=np.uint8)
+        _check(self.lib.kdpt_write_pbo(self._ctx, int(iteration), out.ctypes.data_as(C.POINTER(C.c_uint8))),
+               "kdpt_write_pbo")
+        return out
+
+    def reset(self):
+        _check(self.lib.kdpt_reset(self._ctx), "kdpt_reset")
+
+    def stats(self) -> Stats:
+        s = Stats()
+        _check(self.lib.kdpt_get_stats(self._ctx, C.byref(s)), "kdpt_get_stats")
+        return s
+
+    def image_device_ptr(self) -> int:
+        p = C.c_void_p()
+        _check(self.lib.kdpt_image_device_ptr(self._ctx, C.byref(p)), "kdpt_image_device_ptr")
+        return int(p.value or 0)
+
+    def debug_paths(self, iteration: int, stop_depth: int):
+        n = self.width * self.height
+        out = (PathSegment * n)()
+        cnt = C.c_int()
+        _check(self.lib.kdpt_debug_paths(self._ctx, int(iteration), int(stop_depth), out, C.byref(cnt)),
+               "kdpt_debug_paths")
+        return np.frombuffer(bytes(out), dtype=PATH_DTYPE)[: cnt.value].copy()
+
+    def count_iteration(self, iteration: int):
+        out = (C.c_ulonglong * 3)()
+        _check(self.lib.kdpt_count_iteration(self._ctx, int(iteration), out), "kdpt_count_iteration")
+        return int(out[0]), int(out[1]), int(out[2])
+
+    def close(self):
+        if self._ctx:
+            self.lib.kdpt_destroy(self._ctx)
+            self._ctx = C.c_void_p()
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+
+PATH_DTYPE = np.dtype([("origin", "<f4", 3), ("direction", "<f4", 3), ("isinside", "u1"), ("pad", "u1", 3),
+                       ("sdepth", "<f4"), ("color", "<f4", 3), ("pixelIndex", "<i4"), ("remainingBounces", "<i4"),
+                       ("materialIdHit", "<i4")])
+assert PATH_DTYPE.itemsize == 56
+
+
+def imgsum(image: np.ndarray) -> float:
+    """Sum as the survey's anchor table defines it: per-pixel float32 (r+g+b), accumulated in double."""
+    im = np.asarray(image, dtype=np.float32).reshape(-1, 3)
+    per_px = (im[:, 0] + im[:, 1]) + im[:, 2]  # float32 adds, left to right
+    return float(np.sum(per_px.astype(np.float64)))

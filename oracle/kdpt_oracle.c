@@ -1571,15 +1571,15 @@ int orc_load_obj(const char *obj_path, float **verts9_out, float **norms9_out, i
 /* ------------------------------------------------------------------ */
 /* Scene (src/scene.cpp) + runCuda camera (src/main.cpp)                  */
 /* ------------------------------------------------------------------ */
-int orc_load_scene(const char *scene_path, const char *obj_path, int res_w, int res_h, int depth, orc_scene *out) {
-    memset(out, 0, sizeof *out);
+int orc_parse_scene(const char *scene_path, const char *obj_path, orc_scene_desc *d) {
+    memset(d, 0, sizeof *d);
     lreader r;
     if (lr_open(&r, scene_path) != 0) return -1;
-    int gcap = 16, mcap = 16;
-    out->geoms = (orc_geom *)calloc((size_t)gcap, sizeof(orc_geom));
-    out->materials = (orc_material *)calloc((size_t)mcap, sizeof(orc_material));
-    orc_camera *cam = &out->camera;
-    float fovy = 0;
+    int gcap = 16, mcap = 16, ng = 0, nm = 0;
+    orc_material *mats = (orc_material *)calloc((size_t)mcap, sizeof(orc_material));
+    int *gtype = (int *)calloc((size_t)gcap, sizeof(int));
+    int *gmat = (int *)calloc((size_t)gcap, sizeof(int));
+    float *gtrs = (float *)calloc((size_t)gcap * 9, sizeof(float));
     char line[8192], work[8192];
     char *tok[MAXTOK];
     while (!r.eof) {
@@ -1589,8 +1589,9 @@ int orc_load_scene(const char *scene_path, const char *obj_path, int res_w, int 
         int nt = tokenize(work, tok);
         if (nt == 0) continue;
         if (strcmp(tok[0], "MATERIAL") == 0 && nt > 1) {
+            /* Scene::loadMaterial src/scene.cpp:236-271 */
             int id = atoi(tok[1]);
-            if (id != out->num_materials) continue;
+            if (id != nm) continue;
             orc_material m;
             memset(&m, 0, sizeof m);
             for (int i = 0; i < 7; i++) {
@@ -1598,63 +1599,64 @@ int orc_load_scene(const char *scene_path, const char *obj_path, int res_w, int 
                 strcpy(work, line);
                 int n2 = tokenize(work, tok);
                 if (n2 == 0) continue;
-                if (strcmp(tok[0], "RGB") == 0) { for (int c = 0; c < 3; c++) m.color[c] = (float)atof(tok[1 + c]); }
-                else if (strcmp(tok[0], "SPECEX") == 0) m.spec_exponent = (float)atof(tok[1]);
-                else if (strcmp(tok[0], "SPECRGB") == 0) { for (int c = 0; c < 3; c++) m.spec_color[c] = (float)atof(tok[1 + c]); }
-                else if (strcmp(tok[0], "REFL") == 0) m.hasReflective = (float)atof(tok[1]);
-                else if (strcmp(tok[0], "REFR") == 0) m.hasRefractive = (float)atof(tok[1]);
-                else if (strcmp(tok[0], "REFRIOR") == 0) m.indexOfRefraction = (float)atof(tok[1]);
-                else if (strcmp(tok[0], "EMITTANCE") == 0) m.emittance = (float)atof(tok[1]);
+                if (strcmp(tok[0], "RGB") == 0 && n2 >= 4) { for (int c = 0; c < 3; c++) m.color[c] = (float)atof(tok[1 + c]); }
+                else if (strcmp(tok[0], "SPECEX") == 0 && n2 >= 2) m.spec_exponent = (float)atof(tok[1]);
+                else if (strcmp(tok[0], "SPECRGB") == 0 && n2 >= 4) { for (int c = 0; c < 3; c++) m.spec_color[c] = (float)atof(tok[1 + c]); }
+                else if (strcmp(tok[0], "REFL") == 0 && n2 >= 2) m.hasReflective = (float)atof(tok[1]);
+                else if (strcmp(tok[0], "REFR") == 0 && n2 >= 2) m.hasRefractive = (float)atof(tok[1]);
+                else if (strcmp(tok[0], "REFRIOR") == 0 && n2 >= 2) m.indexOfRefraction = (float)atof(tok[1]);
+                else if (strcmp(tok[0], "EMITTANCE") == 0 && n2 >= 2) m.emittance = (float)atof(tok[1]);
             }
-            if (out->num_materials == mcap) { mcap *= 2; out->materials = (orc_material *)realloc(out->materials, sizeof(orc_material) * (size_t)mcap); }
-            out->materials[out->num_materials++] = m;
+            if (nm == mcap) { mcap *= 2; mats = (orc_material *)realloc(mats, sizeof(orc_material) * (size_t)mcap); }
+            mats[nm++] = m;
         } else if (strcmp(tok[0], "OBJECT") == 0 && nt > 1) {
+            /* Scene::loadGeom src/scene.cpp:118-173 */
             int id = atoi(tok[1]);
-            if (id != out->num_geoms) continue;
-            orc_geom g;
-            memset(&g, 0, sizeof g);
-            g.type = -1;
+            if (id != ng) continue;
+            int type = -1, matid = 0;
             lr_getline(&r, line, sizeof line);
             if (line[0] && !r.eof) {
-                if (strcmp(line, "sphere") == 0) g.type = 0;
-                else if (strcmp(line, "cube") == 0) g.type = 1;
+                if (strcmp(line, "sphere") == 0) type = 0;
+                else if (strcmp(line, "cube") == 0) type = 1;
             }
             lr_getline(&r, line, sizeof line);
             if (line[0] && !r.eof) {
                 strcpy(work, line);
                 int n2 = tokenize(work, tok);
-                if (n2 > 1) g.materialid = atoi(tok[1]);
+                if (n2 > 1) matid = atoi(tok[1]);
             }
-            v3 T = V3(0, 0, 0), R = V3(0, 0, 0), S = V3(0, 0, 0);
+            float trs[9] = {0};
             lr_getline(&r, line, sizeof line);
             while (line[0] && !r.eof) {
                 strcpy(work, line);
                 int n2 = tokenize(work, tok);
                 if (n2 >= 4) {
-                    v3 vv = V3((float)atof(tok[1]), (float)atof(tok[2]), (float)atof(tok[3]));
-                    if (strcmp(tok[0], "TRANS") == 0) T = vv;
-                    else if (strcmp(tok[0], "ROTAT") == 0) R = vv;
-                    else if (strcmp(tok[0], "SCALE") == 0) S = vv;
+                    float vv[3] = {(float)atof(tok[1]), (float)atof(tok[2]), (float)atof(tok[3])};
+                    if (strcmp(tok[0], "TRANS") == 0) memcpy(trs, vv, 12);
+                    else if (strcmp(tok[0], "ROTAT") == 0) memcpy(trs + 3, vv, 12);
+                    else if (strcmp(tok[0], "SCALE") == 0) memcpy(trs + 6, vv, 12);
                 }
                 lr_getline(&r, line, sizeof line);
             }
-            memcpy(g.translation, &T, 12); memcpy(g.rotation, &R, 12); memcpy(g.scale, &S, 12);
-            m4 tr = buildTransformationMatrix(T, R, S);
-            m4 inv = m4inverse(&tr);
-            m4 it = m4inverseTranspose(&tr);
-            memcpy(g.transform, &tr, 64); memcpy(g.inverseTransform, &inv, 64); memcpy(g.invTranspose, &it, 64);
-            if (out->num_geoms == gcap) { gcap *= 2; out->geoms = (orc_geom *)realloc(out->geoms, sizeof(orc_geom) * (size_t)gcap); }
-            out->geoms[out->num_geoms++] = g;
+            if (ng == gcap) {
+                gcap *= 2;
+                gtype = (int *)realloc(gtype, sizeof(int) * (size_t)gcap);
+                gmat = (int *)realloc(gmat, sizeof(int) * (size_t)gcap);
+                gtrs = (float *)realloc(gtrs, sizeof(float) * 9 * (size_t)gcap);
+            }
+            gtype[ng] = type; gmat[ng] = matid; memcpy(gtrs + 9 * ng, trs, sizeof trs);
+            ng++;
         } else if (strcmp(tok[0], "CAMERA") == 0) {
+            /* Scene::loadCamera src/scene.cpp:175-234 */
             for (int i = 0; i < 5; i++) {
                 lr_getline(&r, line, sizeof line);
                 strcpy(work, line);
                 int n2 = tokenize(work, tok);
                 if (n2 == 0) continue;
-                if (strcmp(tok[0], "RES") == 0) { cam->resolution[0] = atoi(tok[1]); cam->resolution[1] = atoi(tok[2]); }
-                else if (strcmp(tok[0], "FOVY") == 0) fovy = (float)atof(tok[1]);
-                else if (strcmp(tok[0], "ITERATIONS") == 0) out->iterations = atoi(tok[1]);
-                else if (strcmp(tok[0], "DEPTH") == 0) out->traceDepth = atoi(tok[1]);
+                if (strcmp(tok[0], "RES") == 0 && n2 >= 3) { d->res[0] = atoi(tok[1]); d->res[1] = atoi(tok[2]); }
+                else if (strcmp(tok[0], "FOVY") == 0 && n2 >= 2) d->fovy = (float)atof(tok[1]);
+                else if (strcmp(tok[0], "ITERATIONS") == 0 && n2 >= 2) d->iterations = atoi(tok[1]);
+                else if (strcmp(tok[0], "DEPTH") == 0 && n2 >= 2) d->traceDepth = atoi(tok[1]);
             }
             lr_getline(&r, line, sizeof line);
             while (line[0] && !r.eof) {
@@ -1662,32 +1664,70 @@ int orc_load_scene(const char *scene_path, const char *obj_path, int res_w, int 
                 int n2 = tokenize(work, tok);
                 if (n2 >= 4) {
                     float vv[3] = {(float)atof(tok[1]), (float)atof(tok[2]), (float)atof(tok[3])};
-                    if (strcmp(tok[0], "EYE") == 0) memcpy(cam->position, vv, 12);
-                    else if (strcmp(tok[0], "LOOKAT") == 0) memcpy(cam->lookAt, vv, 12);
-                    else if (strcmp(tok[0], "UP") == 0) memcpy(cam->up, vv, 12);
+                    if (strcmp(tok[0], "EYE") == 0) memcpy(d->eye, vv, 12);
+                    else if (strcmp(tok[0], "LOOKAT") == 0) memcpy(d->lookAt, vv, 12);
+                    else if (strcmp(tok[0], "UP") == 0) memcpy(d->up, vv, 12);
                 }
                 lr_getline(&r, line, sizeof line);
             }
-            cam->fov[1] = fovy;
-            v3 view = vnormalize(vsub(V3(cam->lookAt[0], cam->lookAt[1], cam->lookAt[2]),
-                                      V3(cam->position[0], cam->position[1], cam->position[2])));
-            memcpy(cam->view, &view, 12);
         }
     }
     free(r.buf);
-    if (res_w > 0 && res_h > 0) { cam->resolution[0] = res_w; cam->resolution[1] = res_h; }
-    if (depth > 0) out->traceDepth = depth;
-    /* loadCamera fov / pixelLength (src/scene.cpp:215-223) */
-    {
+    d->num_materials = nm; d->materials = mats;
+    d->num_geoms = ng; d->geom_type = gtype; d->geom_material = gmat; d->geom_trs = gtrs;
+    if (obj_path && obj_path[0]) {
+        float *V9, *N9;
+        int *S, ntri, nsh;
+        orc_material *M;
+        if (orc_load_obj(obj_path, &V9, &N9, &S, &ntri, &M, &nsh) != 0) return -2;
+        d->ntri = ntri; d->verts9 = V9; d->norms9 = N9; d->shape_of_tri = S;
+        d->num_shapes = nsh; d->shape_materials = M;
+    }
+    return 0;
+}
+
+void orc_free_desc(orc_scene_desc *d) {
+    free((void *)d->materials); free((void *)d->geom_type); free((void *)d->geom_material); free((void *)d->geom_trs);
+    free((void *)d->verts9); free((void *)d->norms9); free((void *)d->shape_of_tri); free((void *)d->shape_materials);
+    memset(d, 0, sizeof *d);
+}
+
+int orc_build_scene(const orc_scene_desc *d, orc_scene *out) {
+    memset(out, 0, sizeof *out);
+    orc_camera *cam = &out->camera;
+    out->iterations = d->iterations;
+    out->traceDepth = d->traceDepth;
+    int nm = d->num_materials + (d->ntri > 0 ? d->num_shapes : 0);
+    out->materials = (orc_material *)calloc((size_t)(nm > 0 ? nm : 1), sizeof(orc_material));
+    memcpy(out->materials, d->materials, sizeof(orc_material) * (size_t)d->num_materials);
+    out->num_materials = d->num_materials;
+    out->geoms = (orc_geom *)calloc((size_t)(d->num_geoms > 0 ? d->num_geoms : 1), sizeof(orc_geom));
+    out->num_geoms = d->num_geoms;
+    for (int i = 0; i < d->num_geoms; i++) {
+        orc_geom *g = &out->geoms[i];
+        g->type = d->geom_type[i];
+        g->materialid = d->geom_material[i];
+        const float *trs = d->geom_trs + 9 * i;
+        memcpy(g->translation, trs, 12); memcpy(g->rotation, trs + 3, 12); memcpy(g->scale, trs + 6, 12);
+        m4 tr = buildTransformationMatrix(V3(trs[0], trs[1], trs[2]), V3(trs[3], trs[4], trs[5]), V3(trs[6], trs[7], trs[8]));
+        m4 inv = m4inverse(&tr);
+        m4 it = m4inverseTranspose(&tr);
+        memcpy(g->transform, &tr, 64); memcpy(g->inverseTransform, &inv, 64); memcpy(g->invTranspose, &it, 64);
+    }
+    cam->resolution[0] = d->res[0]; cam->resolution[1] = d->res[1];
+    memcpy(cam->position, d->eye, 12); memcpy(cam->lookAt, d->lookAt, 12); memcpy(cam->up, d->up, 12);
+    float fovy = d->fovy;
+    {   /* loadCamera fov / pixelLength / view (src/scene.cpp:215-225) */
         float yscaled = tanf(fovy * (PI_F / 180.0f));
         float xscaled = (yscaled * (float)cam->resolution[0]) / (float)cam->resolution[1];
         float fovx = (atanf(xscaled) * 180.0f) / PI_F;
         cam->fov[0] = fovx; cam->fov[1] = fovy;
         cam->pixelLength[0] = 2 * xscaled / (float)cam->resolution[0];
         cam->pixelLength[1] = 2 * yscaled / (float)cam->resolution[1];
+        v3 view = vnormalize(vsub(V3(d->lookAt[0], d->lookAt[1], d->lookAt[2]), V3(d->eye[0], d->eye[1], d->eye[2])));
+        memcpy(cam->view, &view, 12);
     }
-    /* main(): phi/theta/zoom (src/main.cpp:1059-1073) then runCuda (src/main.cpp:1111-1129) */
-    {
+    {   /* main(): phi/theta/zoom (src/main.cpp:1059-1073) then runCuda (src/main.cpp:1111-1129) */
         v3 view = V3(cam->view[0], cam->view[1], cam->view[2]);
         v3 pos = V3(cam->position[0], cam->position[1], cam->position[2]);
         v3 look = V3(cam->lookAt[0], cam->lookAt[1], cam->lookAt[2]);
@@ -1707,23 +1747,30 @@ int orc_load_scene(const char *scene_path, const char *obj_path, int res_w, int 
         cp = vadd(cp, vadd(look, camoffset));
         memcpy(cam->position, &cp, 12);
     }
-    if (obj_path && obj_path[0]) {
-        float *V9, *N9;
-        int *S, ntri, nsh;
-        orc_material *M;
-        if (orc_load_obj(obj_path, &V9, &N9, &S, &ntri, &M, &nsh) != 0) return -2;
+    if (d->ntri > 0) {
+        int nsh = d->num_shapes;
         out->num_shapes = nsh;
         out->obj_materialOffsets = (int *)calloc((size_t)(nsh > 0 ? nsh : 1), sizeof(int));
         for (int i = 0; i < nsh; i++) {
             out->obj_materialOffsets[i] = out->num_materials;
-            if (out->num_materials == mcap) { mcap *= 2; out->materials = (orc_material *)realloc(out->materials, sizeof(orc_material) * (size_t)mcap); }
-            out->materials[out->num_materials++] = M[i];
+            out->materials[out->num_materials++] = d->shape_materials[i];
         }
-        orc_build_kd(V9, N9, S, ntri, 13, &out->nodes, &out->num_nodes, &out->tris, &out->num_tris);
+        orc_build_kd(d->verts9, d->norms9, d->shape_of_tri, d->ntri, 13, &out->nodes, &out->num_nodes, &out->tris,
+                     &out->num_tris);
         out->has_obj = 1;
-        free(V9); free(N9); free(S); free(M);
     }
     return 0;
+}
+
+int orc_load_scene(const char *scene_path, const char *obj_path, int res_w, int res_h, int depth, orc_scene *out) {
+    orc_scene_desc d;
+    int rc = orc_parse_scene(scene_path, obj_path, &d);
+    if (rc) { orc_free_desc(&d); return rc; }
+    if (res_w > 0 && res_h > 0) { d.res[0] = res_w; d.res[1] = res_h; }
+    if (depth > 0) d.traceDepth = depth;
+    rc = orc_build_scene(&d, out);
+    orc_free_desc(&d);
+    return rc;
 }
 
 void orc_free_scene(orc_scene *s) {

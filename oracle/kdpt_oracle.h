@@ -136,7 +136,38 @@ typedef struct {
     long long seg_per_bounce[32];
 } orc_stats;
 
+/* A parsed-but-unbuilt scene: exactly the values the reference's parsers
+ * produce (scene text: src/scene.cpp:118-271; OBJ: tinyobjloader) before any
+ * matrix, camera or KD work.  Fixtures under tests/golden/ store this form. */
+typedef struct {
+    int res[2];
+    float fovy;
+    int iterations;
+    int traceDepth;
+    float eye[3], lookAt[3], up[3];
+    int num_materials;
+    const orc_material *materials;
+    int num_geoms;
+    const int *geom_type;      /* per geom: 0 sphere, 1 cube */
+    const int *geom_material;  /* per geom */
+    const float *geom_trs;     /* per geom: translation[3], rotation[3], scale[3] */
+    int ntri;                  /* 0: no OBJ */
+    const float *verts9, *norms9;
+    const int *shape_of_tri;
+    int num_shapes;
+    const orc_material *shape_materials;
+} orc_scene_desc;
+
 void orc_default_opts(orc_opts *o);
+
+/* Build matrices (src/utilities.cpp:256-263, glm inverse/inverseTranspose),
+ * the loadCamera/runCuda camera and the KD tree (split(13)) from a desc. */
+int orc_build_scene(const orc_scene_desc *d, orc_scene *out);
+
+/* Parse scene text (+ optional OBJ) into a desc; arrays are malloc'd and must
+ * be released with orc_free_desc. */
+int orc_parse_scene(const char *scene_path, const char *obj_path, orc_scene_desc *d);
+void orc_free_desc(orc_scene_desc *d);
 
 /* Scene text (src/scene.cpp:7-271) + optional OBJ (src/scene.cpp:579-968) +
  * the runCuda camera (src/main.cpp:1059-1073,1111-1129).  res_w/res_h/depth

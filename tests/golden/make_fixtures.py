@@ -1,0 +1,101 @@
+"""Generate the committed fixtures from the reference's own data files.
+
+Run here (where /root/reference exists):  python tests/golden/make_fixtures.py
+Writes:
+  scenes/<name>.json   parsed scene text (Scene::loadMaterial/loadGeom/loadCamera values)
+  meshes/<name>.npz    parsed OBJ (tinyobjloader values, triangles as Scene::loadObj lists them)
+  anchors.json         pins: survey anchor table (reference kernels run host-side),
+                       sha256 of NodeBare[]/TriBare[] from oracle/_ref (the reference's
+                       own KDnode.cpp/KDtree.cpp/tiny_obj_loader.cpp), Houdini KAT hash.
+The parsing uses the oracle (oracle/liboracle.so); parity of the product's own
+C++ parsers with it is checked by tests/test_host_builder.py.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import sys
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(os.path.dirname(HERE)))
+sys.path.insert(0, os.path.dirname(HERE))
+
+import oracle_lib  # noqa: E402
+from kdtreepathtraceroptimization_amd.runtime import MATERIAL_DTYPE  # noqa: E402
+
+REF = "/root/reference"
+SCENES = {"cornell": "scenes/cornell.txt", "cornell8": "scenes/cornell8.txt"}
+MESHES = {"sphere_low_1": "scenes/sphere_low_1.obj", "dragon_5": "scenes/dragon_5.obj"}
+
+
+def f32(x):
+    return float(np.float32(x))
+
+
+def mat_json(m):
+    return {k: ([f32(v) for v in m[k]] if np.ndim(m[k]) else f32(m[k])) for k in MATERIAL_DTYPE.names}
+
+
+def main():
+    oracle_lib.build()
+    os.makedirs(os.path.join(HERE, "scenes"), exist_ok=True)
+    os.makedirs(os.path.join(HERE, "meshes"), exist_ok=True)
+    for name, rel in SCENES.items():
+        d = oracle_lib.parse_reference_scene(os.path.join(REF, rel))
+        js = {"source": rel, "res": [int(d.res[0]), int(d.res[1])], "fovy": f32(d.fovy),
+              "iterations": int(d.iterations), "depth": int(d.trace_depth),
+              "eye": [f32(v) for v in d.eye], "lookAt": [f32(v) for v in d.look_at], "up": [f32(v) for v in d.up],
+              "materials": [mat_json(m) for m in d.materials],
+              "geoms": [{"type": int(t), "material": int(m), "trs": [f32(v) for v in trs]}
+                        for t, m, trs in zip(d.geom_type, d.geom_material, d.geom_trs)]}
+        with open(os.path.join(HERE, "scenes", f"{name}.json"), "w") as f:
+            json.dump(js, f, indent=1)
+    for name, rel in MESHES.items():
+        d = oracle_lib.parse_reference_scene(os.path.join(REF, "scenes/cornell.txt"), os.path.join(REF, rel))
+        np.savez_compressed(os.path.join(HERE, "meshes", f"{name}.npz"), verts9=d.verts9, norms9=d.norms9,
+                            shape_of_tri=d.shape_of_tri,
+                            shape_materials=np.frombuffer(d.shape_materials.tobytes(), np.float32),
+                            source=np.array(rel))
+    # --- pins
+    anchors = {"survey_anchor_table": [
+        {"scene": "cornell", "mesh": None, "res": [64, 64], "depth": 2, "iters": [1, 1], "segments": 7506,
+         "imgsum": 5326.331449},
+        {"scene": "cornell", "mesh": "sphere_low_1", "res": [800, 800], "depth": 8, "iters": [1, 1],
+         "segments": 2450023, "imgsum": 394839.568014},
+        {"scene": "cornell", "mesh": "dragon_5", "res": [800, 800], "depth": 8, "iters": [1, 1],
+         "segments": 2506597, "imgsum": 354095.106512},
+        {"scene": "cornell", "mesh": "dragon_5", "res": [200, 200], "depth": 8, "iters": [1, 2],
+         "segments": 312548, "imgsum": 44569.181530}],
+        "survey_anchor_note": "SURVEY.md 8(c): reference kernels compiled host-only and run in the survey "
+                              "container; imgsum = sum over pixels of float32(r+g+b) accumulated in double",
+        "kd_sha256": {}, "survey_kd_sha256_prefix_suffix": {
+            "sphere_low_1": {"nodes": ["0dcea825", "cf88b346"], "tris": ["64a16dec", "95ca3739"]},
+            "dragon_5": {"nodes": ["2ef8179d", "ee248344"], "tris": ["36daf4c1", "c400eeae"]}}}
+    subprocess.run(["make", "-s", "-C", os.path.join(os.path.dirname(HERE), "..", "oracle", "ref")], check=True)
+    with tempfile.TemporaryDirectory() as td:
+        for name, rel in MESHES.items():
+            n, t = os.path.join(td, "n.bin"), os.path.join(td, "t.bin")
+            subprocess.run([oracle_lib.REF_KD, "obj", os.path.join(REF, rel), n, t], check=True,
+                           stdout=subprocess.DEVNULL)
+            anchors["kd_sha256"][name] = {"nodes": hashlib.sha256(open(n, "rb").read()).hexdigest(),
+                                          "tris": hashlib.sha256(open(t, "rb").read()).hexdigest(),
+                                          "num_nodes": os.path.getsize(n) // 64, "num_tris": os.path.getsize(t) // 76}
+        kat = os.path.join(td, "kat.txt")
+        subprocess.run([oracle_lib.REF_KD, "kat", os.path.join(REF, "rnd/houdini/data"), "30", kat], check=True)
+        expect = open(os.path.join(REF, "rnd/houdini/dataout"), "rb").read().replace(b"\r", b"")
+        assert open(kat, "rb").read() == expect, "oracle/_ref does not reproduce rnd/houdini/dataout"
+        anchors["houdini_kat"] = {"maxdepth": 30, "dataout_sha256_no_cr": hashlib.sha256(expect).hexdigest(),
+                                  "lines": expect.count(b"\n")}
+    # Houdini KAT input (720 triangles, atof -> float) as a fixture
+    vals = [np.float32(float(x)) for x in open(os.path.join(REF, "rnd/houdini/data")).read().split()]
+    np.save(os.path.join(HERE, "houdini_kat_triangles.npy"), np.array(vals, np.float32).reshape(-1, 9))
+    with open(os.path.join(HERE, "anchors.json"), "w") as f:
+        json.dump(anchors, f, indent=1)
+    print("fixtures written")
+
+
+if __name__ == "__main__":
+    main()
