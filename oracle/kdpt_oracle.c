@@ -738,6 +738,36 @@ static void traceOneBounce(const orc_scene *s, const orc_opts *o, int depth, int
     tot->aabb += ca; tot->tri += ct; tot->hit += ch;
 }
 
+int orc_trace_ray(const orc_scene *s, const float *origin, const float *direction, int hybrid, double *out) {
+    unsigned char *visited = (unsigned char *)malloc((size_t)s->num_nodes + 1);
+    counters_t cnt = {0, 0, 0};
+    ray_t ray;
+    ray.origin = V3(origin[0], origin[1], origin[2]);
+    ray.direction = V3(direction[0], direction[1], direction[2]);
+    ray.isinside = 0; ray.sdepth = 0;
+    hitrec_t h;
+    h.t_min = FLT_MAX; h.hit_geom_index = -1; h.obj_intersect = 0; h.objMaterialIdx = -1;
+    h.intersect_point = V3(0, 0, 0); h.normal = V3(0, 0, 0);
+    v3 tmp_i = V3(0, 0, 0), tmp_n = V3(0, 0, 0);
+    int outside = 1;
+    float t = 0;
+    for (int i = 0; i < s->num_geoms; i++) {
+        const orc_geom *g = &s->geoms[i];
+        if (g->type == 1) t = boxIntersectionTest(g, ray, &tmp_i, &tmp_n, &outside);
+        else if (g->type == 0) t = sphereIntersectionTest(g, ray, &tmp_i, &tmp_n, &outside);
+        if (t > 0.0f && h.t_min > t) { h.t_min = t; h.hit_geom_index = i; h.intersect_point = tmp_i; h.normal = tmp_n; }
+    }
+    v3 bary = V3(0, 0, 0);
+    if (s->has_obj) traverseKD(s, ray, &bary, &h, visited, hybrid, s->num_materials, &cnt);
+    out[0] = h.t_min; out[1] = h.hit_geom_index;
+    out[2] = h.intersect_point.x; out[3] = h.intersect_point.y; out[4] = h.intersect_point.z;
+    out[5] = h.normal.x; out[6] = h.normal.y; out[7] = h.normal.z;
+    out[8] = h.obj_intersect; out[9] = h.objMaterialIdx;
+    out[10] = (double)cnt.aabb; out[11] = (double)cnt.tri; out[12] = (double)cnt.hit;
+    free(visited);
+    return 0;
+}
+
 /* src/pathtrace.cu:2304-2369 */
 static void shadeMaterial(const orc_scene *s, const orc_opts *o, int num_paths, const orc_isect *isects,
                           orc_path *paths) {

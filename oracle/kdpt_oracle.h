@@ -205,6 +205,11 @@ int orc_render(const orc_scene *s, const orc_opts *o, int iter_first, int iter_c
 int orc_paths_after(const orc_scene *s, const orc_opts *o, int iter, int stop_depth,
                     orc_path *out, int *npaths);
 
+/* One ray through the geoms + KD traversal of pathTraceOneBounceKDbare (no scatter).
+ * out[0]=t_min out[1]=hit_geom_index out[2..4]=intersect point out[5..7]=normal
+ * out[8]=obj_intersect out[9]=objMaterialIdx out[10..12]=aabb/tri/hit tests. */
+int orc_trace_ray(const orc_scene *s, const float *origin, const float *direction, int hybrid, double *out);
+
 /* Device-math known answers shared with the HIP tests. */
 unsigned int orc_utilhash(unsigned int a);
 float orc_u01_sequence(int iter, int index, int depth, int k); /* k-th uniform */
