@@ -1,0 +1,187 @@
+"""bench.py -- the reference's headline metric on MI355X.
+
+Metric (BASELINE.json): Mrays/s at 800x800, depth 8, cornell + dragon (dragon_5.obj: the
+only dragon mesh present -- cornell9.txt does not exist).
+A step = one iteration = one sample per pixel through the whole hot path
+(camera rays -> up to 8 x [intersect + KD traversal + scatter + shade + gather +
+stable compaction]).  Mrays/s = path segments launched into the intersect kernel,
+summed over all ranks, / the max-over-ranks wall time of the K timed steps.
+
+Multi-GPU (one process per GPU, `torch.distributed.run`): samples per pixel shard
+across ranks (rank r renders global iterations r+1, r+1+N, ...: weak scaling) and the
+float3 accumulation images are summed on rank 0 with one RCCL reduce over xGMI inside
+the timed region.
+
+Roofline: the dominant kernel is the fused bounce kernel (k_bounce); HBM-bound by
+SURVEY.md 8(d): algorithmic bytes per segment B = 352 + 52*N_aabb + 36*N_tri + 40*N_hit
+(counts from an untimed counting iteration), achieved = bytes per launch / average launch
+time measured with HIP events on the kernel's own stream during the timed steps.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+
+
+def parse():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--mesh", default="dragon_5")
+    ap.add_argument("--scene", default="cornell")
+    ap.add_argument("--res", type=int, nargs=2, default=(800, 800))
+    ap.add_argument("--depth", type=int, default=8)
+    ap.add_argument("--bare", action="store_true", help="traverseKDbare instead of the short-stack hybrid")
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    return ap.parse_args()
+
+
+def cpu_baseline(args):
+    """The oracle (plain-C port of the reference path) on this host's cores, bounded sample."""
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    import oracle_lib
+    from kdtreepathtraceroptimization_amd.fixtures import load_fixture_scene
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    s = oracle_lib.OracleScene.from_description(
+        load_fixture_scene(args.scene, args.mesh, res=tuple(args.res), depth=args.depth))
+    seg, t, it = 0, 0.0, 3
+    while t < args.cpu_seconds and it < 3 + 64:
+        t0 = time.perf_counter()
+        _, st = s.render(it, 1, nthreads=threads, shortstack=0 if args.bare else 1)
+        t += time.perf_counter() - t0
+        seg += st.segments
+        it += 1
+    return {"value": round(seg / t / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "sample": f"oracle (plain-C restatement of the reference's host-side kernels), {it - 3} iteration(s) "
+                      f"3..{it - 1} of the same workload, {t:.1f} s, OpenMP over paths"}
+
+
+def main():
+    args = parse()
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    import torch
+    dist = None
+    if world > 1:
+        import torch.distributed as dist
+        torch.cuda.set_device(local)
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+    else:
+        torch.cuda.set_device(local)
+    from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options, load_fixture_scene
+
+    desc = load_fixture_scene(args.scene, args.mesh, res=tuple(args.res), depth=args.depth)
+    sd = SceneData.from_description(desc)
+    W, H = sd.resolution
+    accum = torch.zeros(3 * W * H, dtype=torch.float32, device=f"cuda:{local}")
+    opt = default_options(testing_mode=1, short_stack=0 if args.bare else 1, external_image=accum.data_ptr())
+    pt = PathTracer(sd, opt, device=local)
+
+    def global_iter(step):  # 1-based, distinct across ranks and steps
+        return 1 + step * world + rank
+
+    # warmup (iterations disjoint from the timed ones); iteration 2's extra sort lands here
+    for w in range(args.warmup):
+        pt.trace_iteration(global_iter(w))
+    # roofline counters from one untimed counting iteration of the timed range
+    aabb, tri, hit = pt.count_iteration(global_iter(args.warmup))
+    cnt_stats = pt.stats()
+    accum.zero_()
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    seg = 0
+    kernel_ms = 0.0
+    launches = 0
+    for k in range(args.steps):
+        pt.trace_iteration(global_iter(args.warmup + k))
+        st = pt.stats()
+        seg += st.segments
+        kernel_ms += st.ms_intersect
+        launches += st.bounces
+    if dist:
+        dist.reduce(accum, dst=0)  # spp shards -> one framebuffer (the only exchange step)
+    torch.cuda.synchronize()
+    if dist:
+        dist.barrier()
+    torch.cuda.synchronize()
+    dt = time.perf_counter() - t0
+    if dist:
+        t = torch.tensor([dt, float(seg), kernel_ms, float(launches)], dtype=torch.float64, device=f"cuda:{local}")
+        tmax = t[0:1].clone()
+        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
+        tsum = t[1:].clone()
+        dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
+        dt, seg, kernel_ms, launches = float(tmax[0]), int(tsum[0]), float(tsum[1]), int(tsum[2])
+    if rank != 0:
+        pt.close()
+        if dist:
+            dist.destroy_process_group()
+        return
+    # roofline of the dominant kernel (k_bounce), per launch
+    # counting iteration: aabb/tri/hit for its segments
+    count_seg = max(1, sum(cnt_stats.seg_per_bounce[d] for d in range(32)) or seg // max(1, args.steps * world))
+    per_seg_bytes = 352 + 52 * aabb / count_seg + 36 * tri / count_seg + 40 * hit / count_seg
+    avg_launch_ms = kernel_ms / max(1, launches)
+    seg_per_launch = seg / max(1, launches)
+    bytes_per_launch = per_seg_bytes * seg_per_launch
+    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
+    traffic = None
+    tfile = os.path.join(ROOT, "profiles", f"traffic_{args.scene}_{args.mesh}_{W}x{H}.json")
+    if os.path.exists(tfile):
+        traffic = json.load(open(tfile)).get("hbm_bytes_per_launch")
+    out = {
+        "metric": METRIC,
+        "value": round(seg / dt / 1e6, 3),
+        "unit": "Mrays/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": round(dt * 1e3 / args.steps, 4),
+        "higher_is_better": True,
+        "scaling": "weak",
+        "vs_baseline": None,
+        "dtype": "f32",
+        "data": "synthetic camera rays over the reference's own scene assets (cornell.txt + dragon_5.obj, "
+                "parsed fixtures under tests/golden); deterministic RNG seeded by iteration",
+        "config": {"workload": f"{args.scene}.txt + {args.mesh}.obj, {W}x{H}, depth {args.depth}, 1 spp per step "
+                               f"per GPU, short-stack hybrid KD traversal" if not args.bare else "bare traversal",
+                   "scene": args.scene, "mesh": args.mesh, "resolution": [W, H], "depth": args.depth,
+                   "kd_nodes": sd.view.num_nodes, "kd_tri_refs": sd.view.num_tris,
+                   "parallelism": f"spp-sharded x{world} + RCCL reduce" if world > 1 else "single GPU"},
+        "segments_per_step": seg / (args.steps * world),
+        "primary_rays_per_s": round(W * H * args.steps * world / dt, 1),
+        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                     "kernel": "k_bounce (intersect + KD traversal + scatter + shade + gather)",
+                     "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
+                     "bytes_per_segment": round(per_seg_bytes, 2),
+                     "per_segment_counts": {"aabb": round(aabb / count_seg, 4), "tri": round(tri / count_seg, 4),
+                                            "hit": round(hit / count_seg, 5)}},
+        "reference_980m_intersect_ms_per_iter": 79.4,
+        "intersect_ms_per_iter": round(kernel_ms / (args.steps * world), 4),
+    }
+    if world == 1 and not args.no_cpu_baseline:
+        out["cpu_baseline"] = cpu_baseline(args)
+    pt.close()
+    if dist:
+        dist.destroy_process_group()
+    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -133,6 +133,7 @@ struct BounceArgs {
   int ntiles;
   int nkeys;
   Counters* counters;
+  unsigned long long* total_segments;  // running sum of paths launched into this kernel
 };
 
 template <bool HYBRID, bool COMPACT, bool SORT, bool COUNT>
@@ -141,6 +142,7 @@ __global__ __launch_bounds__(TILE) void k_bounce(BounceArgs A) {
   const int tile = blockIdx.x;
   if (tile * TILE >= n) return;  // uniform per block
   const int i = tile * TILE + threadIdx.x;
+  if (i == 0) atomicAdd(A.total_segments, (unsigned long long)n);
   __shared__ int s_hist[MAX_KEYS];
   __shared__ unsigned int s_cnt[3];
   if (SORT) {
@@ -434,6 +436,7 @@ struct kdpt_ctx {
   int* tile_counts = nullptr;
   int* tile_off = nullptr;
   Counters* counters = nullptr;
+  unsigned long long* total_segments = nullptr;  // device running total (async use)
   int* h_counts = nullptr;  // pinned
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> bounce_ev;
@@ -650,7 +653,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     return bail(rc);
   }
   if ((rc = dalloc(c, &c->counts, c->cap + 2)) || (rc = dalloc(c, &c->tile_counts, (size_t)MAX_KEYS * c->ntiles)) ||
-      (rc = dalloc(c, &c->tile_off, (size_t)MAX_KEYS * c->ntiles)) || (rc = dalloc(c, &c->counters, 1)))
+      (rc = dalloc(c, &c->tile_off, (size_t)MAX_KEYS * c->ntiles)) || (rc = dalloc(c, &c->counters, 1)) ||
+      (rc = dalloc(c, &c->total_segments, 1)))
     return bail(rc);
   if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 2), hipHostMallocDefault) != hipSuccess)
     return bail(fail(KDPT_ERR_HIP, "hipHostMalloc"));
@@ -668,6 +672,7 @@ int kdpt_reset(kdpt_ctx* c) {
   if (!c) return fail(KDPT_ERR_ARG, "null ctx");
   HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipMemsetAsync(c->image, 0, sizeof(float) * 3 * (size_t)c->npix, c->stream));
+  HIP_TRY(hipMemsetAsync(c->total_segments, 0, sizeof(unsigned long long), c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   memset(&c->stats, 0, sizeof c->stats);
   return KDPT_OK;
@@ -712,7 +717,6 @@ int kdpt_trace_iteration(kdpt_ctx* c, int frame, int iter) {
   }
   c->stats.segments = seg;
   c->stats.bounces = bounces;
-  c->stats.total_segments += seg;
   if (c->opt.testing_mode) {
     float tot = 0;
     for (int d = 0; d < bounces; d++) {
@@ -747,6 +751,11 @@ int kdpt_write_pbo(kdpt_ctx* c, int iter, uint8_t* rgba) {
 
 int kdpt_get_stats(kdpt_ctx* c, kdpt_stats* st) {
   if (!c || !st) return fail(KDPT_ERR_ARG, "null arg");
+  HIP_TRY(hipSetDevice(c->device));
+  unsigned long long tot = 0;
+  HIP_TRY(hipMemcpyAsync(&tot, c->total_segments, sizeof tot, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  c->stats.total_segments = (long long)tot;
   *st = c->stats;
   return KDPT_OK;
 }
@@ -759,15 +768,15 @@ int kdpt_image_device_ptr(kdpt_ctx* c, void** p) {
 
 int kdpt_destroy(kdpt_ctx* c) {
   if (!c) return KDPT_OK;
-  hipSetDevice(c->device);
-  if (c->stream) hipStreamSynchronize(c->stream);
-  for (void* p : c->allocs) hipFree(p);
-  if (c->h_counts) hipHostFree(c->h_counts);
-  if (c->ev0) hipEventDestroy(c->ev0);
-  if (c->ev1) hipEventDestroy(c->ev1);
+  (void)hipSetDevice(c->device);
+  if (c->stream) (void)hipStreamSynchronize(c->stream);
+  for (void* p : c->allocs) (void)hipFree(p);
+  if (c->h_counts) (void)hipHostFree(c->h_counts);
+  if (c->ev0) (void)hipEventDestroy(c->ev0);
+  if (c->ev1) (void)hipEventDestroy(c->ev1);
   for (auto e : c->bounce_ev)
-    if (e) hipEventDestroy(e);
-  if (c->stream) hipStreamDestroy(c->stream);
+    if (e) (void)hipEventDestroy(e);
+  if (c->stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return KDPT_OK;
 }
@@ -781,9 +790,12 @@ int kdpt_debug_paths(kdpt_ctx* c, int iter, int stop_depth, kdpt_path_segment* o
   HIP_TRY(hipMalloc((void**)&scratch, sizeof(float) * 3 * (size_t)c->npix));
   HIP_TRY(hipMemset(scratch, 0, sizeof(float) * 3 * (size_t)c->npix));
   c->image = scratch;
+  unsigned long long* saved_tot = c->total_segments;
+  c->total_segments = reinterpret_cast<unsigned long long*>(c->counters);  // scratch word
   int rc = launch_iteration(c, iter, stop_depth, false);
+  c->total_segments = saved_tot;
   c->image = saved;
-  if (rc) { hipFree(scratch); return rc; }
+  if (rc) { (void)hipFree(scratch); return rc; }
   kdpt_path_segment* d = nullptr;
   HIP_TRY(hipMalloc((void**)&d, sizeof(kdpt_path_segment) * (size_t)c->npix));
   const int depth_slot = stop_depth + 1;
@@ -795,8 +807,8 @@ int kdpt_debug_paths(kdpt_ctx* c, int iter, int stop_depth, kdpt_path_segment* o
   const int n = c->h_counts[depth_slot];
   *npaths = n;
   HIP_TRY(hipMemcpy(out, d, sizeof(kdpt_path_segment) * (size_t)n, hipMemcpyDeviceToHost));
-  hipFree(d);
-  hipFree(scratch);
+  (void)hipFree(d);
+  (void)hipFree(scratch);
   return KDPT_OK;
 }
 
@@ -810,14 +822,20 @@ int kdpt_count_iteration(kdpt_ctx* c, int iter, unsigned long long* aabb_tri_hit
   HIP_TRY(hipMemset(scratch, 0, sizeof(float) * 3 * (size_t)c->npix));
   HIP_TRY(hipMemset(c->counters, 0, sizeof(Counters)));
   c->image = scratch;
+  unsigned long long* saved_tot = c->total_segments;
+  unsigned long long* scratch_tot = nullptr;
+  HIP_TRY(hipMalloc((void**)&scratch_tot, sizeof(unsigned long long)));
+  c->total_segments = scratch_tot;
   int rc = launch_iteration(c, iter, -1, true);
+  c->total_segments = saved_tot;
   c->image = saved;
   Counters h{};
   if (!rc) {
     HIP_TRY(hipMemcpyAsync(&h, c->counters, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
   }
-  hipFree(scratch);
+  (void)hipFree(scratch);
+  (void)hipFree(scratch_tot);
   aabb_tri_hit[0] = h.aabb;
   aabb_tri_hit[1] = h.tri;
   aabb_tri_hit[2] = h.hit;
@@ -834,7 +852,7 @@ int kdpt_selftest_math(const float* x, int n, float* so, float* co) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpy(so, ds, sizeof(float) * n, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(co, dc, sizeof(float) * n, hipMemcpyDeviceToHost));
-  hipFree(dx); hipFree(ds); hipFree(dc);
+  (void)hipFree(dx); (void)hipFree(ds); (void)hipFree(dc);
   return KDPT_OK;
 }
 
@@ -847,7 +865,7 @@ int kdpt_selftest_rng(const int* iid, int n, int k, float* u) {
   hipLaunchKernelGGL(k_selftest_rng, dim3((n + 255) / 256), dim3(256), 0, 0, di, n, k, du);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpy(u, du, sizeof(float) * n, hipMemcpyDeviceToHost));
-  hipFree(di); hipFree(du);
+  (void)hipFree(di); (void)hipFree(du);
   return KDPT_OK;
 }
 
@@ -860,7 +878,7 @@ int kdpt_selftest_fresnel(const float* cs, int n, float ior, float* f) {
   hipLaunchKernelGGL(k_selftest_fresnel, dim3((n + 255) / 256), dim3(256), 0, 0, dc, n, rr * rr, df);
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpy(f, df, sizeof(float) * n, hipMemcpyDeviceToHost));
-  hipFree(dc); hipFree(df);
+  (void)hipFree(dc); (void)hipFree(df);
   return KDPT_OK;
 }
 
@@ -899,6 +917,7 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
     a.ntiles = c->ntiles;
     a.nkeys = c->nkeys;
     a.counters = c->counters;
+    a.total_segments = c->total_segments;
     if (c->opt.testing_mode) HIP_TRY(hipEventRecord(c->bounce_ev[2 * depth], c->stream));
     const bool hyb = c->opt.short_stack != 0;
     if (hyb) {

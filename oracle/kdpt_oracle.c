@@ -287,6 +287,13 @@ float orc_u01_sequence(int iter, int index, int depth, int k) {
 }
 float orc_sinf(float x) { return sinf(x); }
 float orc_cosf(float x) { return cosf(x); }
+void orc_sincos_array(const float *x, int n, float *s, float *c) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++) { s[i] = sinf(x[i]); c[i] = cosf(x[i]); }
+}
+void orc_u01_array(const int *iid, int n, int k, float *u) {
+    for (int i = 0; i < n; i++) u[i] = orc_u01_sequence(iid[3 * i], iid[3 * i + 1], iid[3 * i + 2], k);
+}
 
 /* ------------------------------------------------------------------ */
 /* Intersections (src/intersections.h)                                  */
@@ -431,6 +438,10 @@ static float getFresnelVal(v3 I, v3 N, float ior) { /* :127-133 */
     float R0 = rr * rr; /* glm::pow(float, 2.0f) -> pow(x, 2) folds to x*x */
     double F = (double)R0 + (double)(1.0f - R0) * pow((double)(1.0f - vdot(N, vneg(I))), 5.0);
     return (float)F;
+}
+void orc_fresnel_array(const float *cosines, int n, float ior, float *f) {
+    /* getFresnelVal(I, N, ior) with N = (0,0,1) and I chosen so dot(N,-I) == cosines[i] exactly */
+    for (int i = 0; i < n; i++) f[i] = getFresnelVal(V3(0.0f, 0.0f, -cosines[i]), V3(0.0f, 0.0f, 1.0f), ior);
 }
 static v3 glm_reflect(v3 I, v3 N) { return vsub(I, vscale(vscale(N, vdot(N, I)), 2.0f)); }
 static v3 glm_refract(v3 I, v3 N, float eta) {
@@ -818,7 +829,10 @@ static int run_iteration(const orc_scene *s, const orc_opts *o, int iter, orc_pa
     const orc_camera *cam = &s->camera;
     int W = cam->resolution[0], H = cam->resolution[1];
     int pixelcount = W * H;
-    generateRayFromCamera(cam, iter, s->traceDepth, paths, o->focalLength, o->dofAngle, o->antialias);
+    /* cacherays (src/pathtrace.cu:2448-2456): camera rays of iteration 1 are reused; the
+       bounce RNG still uses the real iter */
+    generateRayFromCamera(cam, o->cacherays ? 1 : iter, s->traceDepth, paths, o->focalLength, o->dofAngle,
+                          o->antialias);
     int depth = 0;
     int num_paths = pixelcount;
     counters_t cnt = {0, 0, 0};
@@ -914,15 +928,8 @@ int orc_render(const orc_scene *s, const orc_opts *o, int iter_first, int iter_c
     if (!paths || !tmp || !isects) { free(paths); free(tmp); free(isects); return -1; }
     orc_stats local;
     memset(&local, 0, sizeof local);
-    for (int it = iter_first; it < iter_first + iter_count; it++) {
-        if (o->cacherays) {
-            /* cacherays regenerates nothing after iter 1: camera rays are iteration-independent
-               only through the cache; the restatement simply regenerates with iter 1's seed. */
-            int saved = it;
-            (void)saved;
-        }
-        run_iteration(s, o, o->cacherays ? 1 : it, paths, tmp, isects, image, &local, -1, NULL);
-    }
+    for (int it = iter_first; it < iter_first + iter_count; it++)
+        run_iteration(s, o, it, paths, tmp, isects, image, &local, -1, NULL);
     if (stats) *stats = local;
     free(paths); free(tmp); free(isects);
     return 0;

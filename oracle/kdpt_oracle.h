@@ -215,6 +215,11 @@ unsigned int orc_utilhash(unsigned int a);
 float orc_u01_sequence(int iter, int index, int depth, int k); /* k-th uniform */
 float orc_sinf(float x);  /* the libm call the reference makes (glibc) */
 float orc_cosf(float x);
+void orc_sincos_array(const float *x, int n, float *s, float *c);
+/* u01 draws: for each (iter, index, depth) triple, the k-th uniform of makeSeededRandomEngine */
+void orc_u01_array(const int *iid, int n, int k, float *u);
+/* getFresnelVal with dot(N,-I) == cosines[i] */
+void orc_fresnel_array(const float *cosines, int n, float ior, float *f);
 
 #ifdef __cplusplus
 }

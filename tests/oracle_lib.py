@@ -95,6 +95,10 @@ def lib():
         L.orc_sinf.restype = C.c_float
         L.orc_cosf.argtypes = [C.c_float]
         L.orc_cosf.restype = C.c_float
+        L.orc_sincos_array.argtypes = [P(C.c_float), C.c_int, P(C.c_float), P(C.c_float)]
+        L.orc_u01_array.argtypes = [P(C.c_int), C.c_int, C.c_int, P(C.c_float)]
+        L.orc_fresnel_array.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
+        L.orc_trace_ray.argtypes = [P(OScene), P(C.c_float), P(C.c_float), C.c_int, P(C.c_double)]
         _lib = L
     return _lib
 
@@ -236,3 +240,28 @@ def parse_reference_scene(scene_path, obj_path=None):
         return desc
     finally:
         lib().orc_free_desc(C.byref(d))
+
+
+def _fp(a):
+    return a.ctypes.data_as(C.POINTER(C.c_float))
+
+
+def sincos(x: np.ndarray):
+    x = np.ascontiguousarray(x, np.float32)
+    s, c = np.empty_like(x), np.empty_like(x)
+    lib().orc_sincos_array(_fp(x), len(x), _fp(s), _fp(c))
+    return s, c
+
+
+def u01(iid: np.ndarray, k: int):
+    iid = np.ascontiguousarray(iid, np.int32)
+    u = np.empty(len(iid), np.float32)
+    lib().orc_u01_array(iid.ctypes.data_as(C.POINTER(C.c_int)), len(iid), k, _fp(u))
+    return u
+
+
+def fresnel(cosines: np.ndarray, ior: float):
+    c = np.ascontiguousarray(cosines, np.float32)
+    f = np.empty_like(c)
+    lib().orc_fresnel_array(_fp(c), len(c), float(np.float32(ior)), _fp(f))
+    return f
