@@ -25,9 +25,16 @@ ARCH = os.environ.get("KDPT_ARCH", "gfx950")
 COMMON = ["-O3", "-std=c++17", "-fPIC", "-ffp-contract=off", "-fno-fast-math", "-I", os.path.join(ROOT, "include")]
 
 
-def _run(cmd):
+def _run(cmd, log=None):
     print("+", " ".join(cmd), flush=True)
-    subprocess.run(cmd, check=True)
+    if log is None:
+        subprocess.run(cmd, check=True)
+        return
+    with open(log, "w") as f:  # long remark output goes to a file, never through a pipe that may close
+        r = subprocess.run(cmd, stdout=f, stderr=subprocess.STDOUT)
+    if r.returncode != 0:
+        sys.stderr.write(open(log).read()[-4000:])
+        raise subprocess.CalledProcessError(r.returncode, cmd)
 
 
 def _sources():
@@ -49,7 +56,8 @@ def build(force: bool = False, verbose_resources: bool = False) -> str:
     dev_obj = os.path.join(BUILD, "kdpt_runtime.o")
     _run(["g++", *COMMON, "-c", os.path.join(CSRC, "scene_host.cpp"), "-o", host_obj])
     extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose_resources else []
-    _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, *extra, "-c", os.path.join(CSRC, "kdpt_runtime.hip"), "-o", dev_obj])
+    _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, *extra, "-c", os.path.join(CSRC, "kdpt_runtime.hip"), "-o", dev_obj],
+         log=os.path.join(BUILD, "kdpt_runtime.build.log"))
     tmp = LIB + ".tmp"
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, dev_obj, host_obj])
     os.replace(tmp, LIB)

@@ -294,6 +294,230 @@ KDPT_HD void traverseKD(const DevScene& S, const Ray& ray, Hit& h, int material_
   }
 }
 
+#if defined(__HIPCC__) || defined(__HIP__)
+// ---------------------------------------------------------------------------
+// Wave-cooperative form of traverseKD for gfx950 (64-lane waves).
+//
+// The per-ray algorithm and visited state are exactly traverseKD's; only the
+// SIMT schedule changes ("while-while"): a node phase advances every lane until
+// it reaches a leaf whose triangles must be tested (or finishes), then a leaf
+// phase spreads ALL (ray, triangle) pairs of the lanes sitting on leaves over the
+// 64 lanes.  A leaf's triangle tests are independent of each other; their
+// sequential effects are recombined per ray through LDS:
+//   bary.z        = that of the LAST triangle (in leaf order) passing the u/v tests
+//   objMaterialIdx= mtlIdx of the LAST intersected triangle
+//   hit record    = FIRST triangle reaching the minimum t with t > 0 && t_min > t
+//   skip marks    = applied min(#intersected, 2) times (idempotent from the 2nd on)
+// ---------------------------------------------------------------------------
+struct WaveLeafLDS {
+  int pend[64];    // inclusive end of each lane's pair range
+  int tbase[64];   // triangle index = tbase[owner] + pair index
+  float4 od[64];   // ray origin.xyz, direction.x
+  float2 dd[64];   // direction.y, direction.z
+  int lastPass[64];
+  int lastHit[64];
+  int nhit[64];
+  unsigned long long best[64];  // (t bits << 32) | triangle index, min
+};
+
+__device__ inline void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// glm::intersectRayTriangle on (o, d) and triangle i; returns 0 = miss before the u/v
+// tests passed, 1 = passed u/v but t < 0 (bary.z still written), 2 = intersected.
+__device__ inline int tri_test(const DevScene& S, int i, f3 o, f3 d, float& bx, float& by, float& bz) {
+  const float4 tv = S.tv0[i];
+  const float4 e1v = S.te1[i];
+  const float4 e2v = S.te2[i];
+  const f3 v0 = mk3(tv.x, tv.y, tv.z), e1 = mk3(e1v.x, e1v.y, e1v.z), e2 = mk3(e2v.x, e2v.y, e2v.z);
+  const f3 p = cross(d, e2);
+  const float a = dot(e1, p);
+  if (a < FLT_EPS) return 0;
+  const float f = 1.0f / a;
+  const f3 s = sub(o, v0);
+  bx = f * dot(s, p);
+  if (bx < 0.0f) return 0;
+  if (bx > 1.0f) return 0;
+  const f3 q = cross(s, e1);
+  by = f * dot(d, q);
+  if (by < 0.0f) return 0;
+  if (by + bx > 1.0f) return 0;
+  bz = f * dot(e2, q);
+  return (bz >= 0.0f) ? 2 : 1;
+}
+
+template <bool HYBRID>
+__device__ inline float tri_hit_t(const DevScene& S, int i, f3 o, f3 d, float bx, float by, float bz, f3& hit,
+                                  f3& norm) {
+  const float4 n1v = S.tn0[i], n2v = S.tn1[i], n3v = S.tn2[i];
+  const float w0 = 1 - bx - by;
+  norm = normalize(add(add(scl(mk3(n1v.x, n1v.y, n1v.z), w0), scl(mk3(n2v.x, n2v.y, n2v.z), bx)),
+                       scl(mk3(n3v.x, n3v.y, n3v.z), by)));
+  hit = add(add(o, scl(d, bz)), scl(norm, HYBRID ? 0.0001f : 0.00001f));
+  return distance(o, hit);
+}
+
+template <bool HYBRID, bool COUNT>
+__device__ void traverseKD_wave(const DevScene& S, const Ray& ray, bool active, Hit& h, int material_size,
+                                TraverseCounters& cnt, WaveLeafLDS* W) {
+  const int lane = threadIdx.x & 63;
+  const f3 o = ray.origin, d = ray.direction;
+  W->od[lane] = make_float4(o.x, o.y, o.z, d.x);
+  W->dd[lane] = make_float2(d.y, d.z);
+  const f3 invdir = active ? mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z) : mk3(0, 0, 0);
+  int cur = S.root, L = 0;
+  uint32_t cb = 0, ps = 0, g = 0;
+  bool rootv = false, sink = false, hitGeom = false;
+  bool done = !active;
+  float dist = -1.0f, bz = FLT_MAXV;
+  while (true) {
+    // ---------------- node phase ----------------
+    bool leaf = false;
+    int lstart = 0, lsize = 0;
+    bool lfirst = true;
+    while (!done && !leaf) {
+      if (cur == -1) { done = true; break; }
+      const float4 b0 = S.nbox0[cur];
+      const float4 b1 = S.nbox1[cur];
+      const int4 meta = S.nmeta[cur];
+      const int left = fbits(b1.z), right = fbits(b1.w), parent = meta.x;
+      const int lvlbit = (L > 0) ? (2 * (L - 1) + (int)((ps >> (L - 1)) & 1u)) : 0;
+      const bool curVis = (L == 0) ? rootv : (((cb >> lvlbit) & 1u) != 0u);
+      if (!hitGeom && parent == -1 && curVis) { done = true; break; }
+      hitGeom = intersectAABB(o, invdir, b0, b1, dist);
+      if (COUNT) cnt.aabb++;
+      bool up = curVis;
+      if (!curVis) {
+        if (!hitGeom && parent == -1) { done = true; break; }
+        up = (!hitGeom || dist > bz);
+      }
+      if (up) {
+        if (L == 0) rootv = true; else cb |= 1u << lvlbit;
+        if (left == -1) sink = true; else cb |= 1u << (2 * L);
+        if (right == -1) sink = true; else cb |= 1u << (2 * L + 1);
+        cur = parent;
+        L--;
+        continue;
+      }
+      const bool leftFirst = HYBRID ? (comp(d, meta.w) > 0.0f) : true;
+      const uint32_t fside = leftFirst ? 0u : 1u;
+      const int first = leftFirst ? left : right, second = leftFirst ? right : left;
+      int next = -1;
+      uint32_t nside = 0;
+      if (first != -1 && !((cb >> (2 * L + fside)) & 1u)) { next = first; nside = fside; }
+      else if (second != -1 && !((cb >> (2 * L + (fside ^ 1u))) & 1u)) { next = second; nside = fside ^ 1u; }
+      if (next != -1) {
+        ps = (ps & ~(1u << L)) | (nside << L);
+        cb &= ~(3u << (2u * (uint32_t)(L + 1)));
+        if (L == 0 && nside == 0u) cb |= g << 2;
+        L++;
+        cur = next;
+        continue;
+      }
+      if (L == 0) rootv = true; else cb |= 1u << lvlbit;
+      if (meta.z > 0) {
+        leaf = true;
+        lstart = meta.y;
+        lsize = meta.z;
+        lfirst = leftFirst;
+      }
+    }
+    if (!__any(leaf)) break;
+    // ---------------- leaf phase (wave-cooperative) ----------------
+    const int sz = leaf ? lsize : 0;
+    int incl = sz;
+#pragma unroll
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(incl, off);
+      if (lane >= off) incl += y;
+    }
+    const int P = __shfl(incl, 63);
+    W->pend[lane] = incl;
+    W->tbase[lane] = lstart - (incl - sz);
+    W->lastPass[lane] = -1;
+    W->lastHit[lane] = -1;
+    W->nhit[lane] = 0;
+    W->best[lane] = ~0ull;
+    wave_lds_sync();
+    for (int pi = lane; pi < P; pi += 64) {
+      int lo = 0, hi = 63;
+#pragma unroll
+      for (int st = 0; st < 6; st++) {
+        const int mid = (lo + hi) >> 1;
+        if (W->pend[mid] > pi) hi = mid; else lo = mid + 1;
+      }
+      const int owner = lo;
+      const int tri = W->tbase[owner] + pi;
+      const float4 q0 = W->od[owner];
+      const float2 q1 = W->dd[owner];
+      const f3 oo = mk3(q0.x, q0.y, q0.z), dd = mk3(q0.w, q1.x, q1.y);
+      float bx, by, bzk;
+      const int r = tri_test(S, tri, oo, dd, bx, by, bzk);
+      if (r == 0) continue;
+      atomicMax(&W->lastPass[owner], tri);
+      if (r == 1) continue;
+      atomicMax(&W->lastHit[owner], tri);
+      atomicAdd(&W->nhit[owner], 1);
+      f3 hp, nn;
+      const float t = tri_hit_t<HYBRID>(S, tri, oo, dd, bx, by, bzk, hp, nn);
+      if (t > 0.0f) atomicMin(&W->best[owner], ((unsigned long long)f2u(t) << 32) | (unsigned int)tri);
+    }
+    wave_lds_sync();
+    if (leaf) {
+      if (COUNT) cnt.tri += lsize;
+      const int lp = W->lastPass[lane];
+      if (lp >= 0) {
+        float bx, by, bzk;
+        tri_test(S, lp, o, d, bx, by, bzk);
+        bz = bzk;
+      }
+      const int nh = W->nhit[lane];
+      if (nh > 0) {
+        if (COUNT) cnt.hit += nh;
+        const int lh = W->lastHit[lane];
+        h.objMaterialIdx = fbits(S.tv0[lh].w) + material_size - 1;
+        if (HYBRID) {
+          for (int rep = 0; rep < (nh > 1 ? 2 : 1); rep++) {
+            const bool parVis = (L == 0) ? sink
+                                : (L == 1 ? rootv
+                                          : (((cb >> (2 * (L - 2) + (int)((ps >> (L - 2)) & 1u))) & 1u) != 0u));
+            const int b = parVis ? 1 : 0;
+            int target = -1;
+            if (b < S.num_nodes) target = (b == 0) ? (lfirst ? S.n0_right : S.n0_left) : (lfirst ? S.n1_right : S.n1_left);
+            if (target == -1) sink = true;
+            else if (b == 0) cb |= 1u << (lfirst ? 1 : 0);
+            else {
+              const uint32_t bit = lfirst ? 1u : 0u;
+              if (L >= 1 && (ps & 1u) == 0u) cb |= 1u << (2 + bit);
+              else g |= 1u << bit;
+            }
+          }
+        }
+        const unsigned long long best = W->best[lane];
+        if (best != ~0ull) {
+          const float tb = u2f((uint32_t)(best >> 32));
+          const int k = (int)(uint32_t)(best & 0xffffffffu);
+          if (h.t_min > tb) {
+            float bx, by, bzk;
+            tri_test(S, k, o, d, bx, by, bzk);
+            f3 hp, nn;
+            h.t_min = tri_hit_t<HYBRID>(S, k, o, d, bx, by, bzk, hp, nn);
+            h.hit_geom_index = S.obj_material_offsets[fbits(S.tv0[k].w)];
+            h.ip = hp;
+            h.normal = nn;
+            h.obj_intersect = true;
+          }
+        }
+      }
+    }
+    wave_lds_sync();  // the LDS slots are rewritten by the next leaf phase
+  }
+}
+#endif  // HIP
+
 // ---------------- src/interactions.h ----------------
 KDPT_HD f3 calculateRandomDirectionInHemisphere(f3 normal, Rng& rng) {  // :9-41
   float up = sqrtf(u01(rng));

@@ -150,47 +150,56 @@ __global__ __launch_bounds__(TILE) void k_bounce(BounceArgs A) {
   }
   if (COUNT && threadIdx.x < 3) s_cnt[threadIdx.x] = 0;
   if (SORT || COUNT) __syncthreads();
+  __shared__ WaveLeafLDS s_leaf[TILE / 64];
   bool alive = false;
   int key = 0;
   TraverseCounters cnt{0, 0, 0};
-  if (i < n) {
-    const float4 q0 = A.paths.p0[i];
-    const float4 q1 = A.paths.p1[i];
-    float4 q2 = A.paths.p2[i];
-    const int pw = fbits(q1.w);
-    const int pix = pw & 0x7fffffff;
-    Ray ray;
-    ray.origin = mk3(q0.x, q0.y, q0.z);
-    ray.direction = mk3(q1.x, q1.y, q1.z);
-    ray.isinside = (pw >> 31) & 1;
-    ray.sdepth = q0.w;
-    f3 color = mk3(q2.x, q2.y, q2.z);
-    int bounces = fbits(q2.w);
-    int matHit = A.paths.pm[i];
-    bool wrote = false;
-    if (bounces > 0) {
-      const DevScene& S = A.S;
-      Hit h;
-      h.t_min = FLT_MAXV;
-      h.hit_geom_index = -1;
-      h.obj_intersect = false;
-      h.objMaterialIdx = -1;
-      h.ip = mk3(0, 0, 0);
-      h.normal = mk3(0, 0, 0);
-      f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
-      float t = 0;
-      for (int g = 0; g < S.num_geoms; g++) {
-        const DevGeom& G = S.geoms[g];
-        if (G.type == 1) t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
-        else if (G.type == 0) t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
-        if (t > 0.0f && h.t_min > t) {
-          h.t_min = t;
-          h.hit_geom_index = g;
-          h.ip = tmp_i;
-          h.normal = tmp_n;
-        }
+  const bool valid = i < n;
+  float4 q0 = make_float4(0, 0, 0, 0), q1 = make_float4(0, 0, 0, 0), q2 = make_float4(0, 0, 0, 0);
+  int matHit = 0;
+  if (valid) {
+    q0 = A.paths.p0[i];
+    q1 = A.paths.p1[i];
+    q2 = A.paths.p2[i];
+    matHit = A.paths.pm[i];
+  }
+  const int pw = fbits(q1.w);
+  const int pix = pw & 0x7fffffff;
+  Ray ray;
+  ray.origin = mk3(q0.x, q0.y, q0.z);
+  ray.direction = mk3(q1.x, q1.y, q1.z);
+  ray.isinside = (pw >> 31) & 1;
+  ray.sdepth = q0.w;
+  f3 color = mk3(q2.x, q2.y, q2.z);
+  int bounces = fbits(q2.w);
+  const bool active = valid && bounces > 0;
+  const DevScene& S = A.S;
+  Hit h;
+  h.t_min = FLT_MAXV;
+  h.hit_geom_index = -1;
+  h.obj_intersect = false;
+  h.objMaterialIdx = -1;
+  h.ip = mk3(0, 0, 0);
+  h.normal = mk3(0, 0, 0);
+  if (active) {
+    f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
+    float t = 0;
+    for (int g = 0; g < S.num_geoms; g++) {
+      const DevGeom& G = S.geoms[g];
+      if (G.type == 1) t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
+      else if (G.type == 0) t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+      if (t > 0.0f && h.t_min > t) {
+        h.t_min = t;
+        h.hit_geom_index = g;
+        h.ip = tmp_i;
+        h.normal = tmp_n;
       }
-      if (S.has_obj) traverseKD<HYBRID, COUNT>(S, ray, h, S.num_materials, cnt);
+    }
+  }
+  if (S.has_obj && S.num_nodes > 0)  // uniform: every lane of the wave takes part
+    traverseKD_wave<HYBRID, COUNT>(S, ray, active, h, S.num_materials, cnt, &s_leaf[threadIdx.x >> 6]);
+  if (valid) {
+    if (active) {
       float isect_t;
       int isect_mat = 0;
       if (h.hit_geom_index == -1) {
@@ -204,7 +213,11 @@ __global__ __launch_bounds__(TILE) void k_bounce(BounceArgs A) {
         isect_mat = mid;
       }
       shade(isect_t, isect_mat, S.materials, A.enable_sss != 0, ray, color, bounces);
-      wrote = true;
+      A.paths.p0[i] = make_float4(ray.origin.x, ray.origin.y, ray.origin.z, ray.sdepth);
+      A.paths.p1[i] = make_float4(ray.direction.x, ray.direction.y, ray.direction.z,
+                                  ibits(pix | ((ray.isinside ? 1 : 0) << 31)));
+      A.paths.p2[i] = make_float4(color.x, color.y, color.z, ibits(bounces));
+      A.paths.pm[i] = matHit;
     }
     if (COMPACT && bounces == 0) {
       // partialGather: one live path per pixel, so this read-modify-write never collides
@@ -212,13 +225,6 @@ __global__ __launch_bounds__(TILE) void k_bounce(BounceArgs A) {
       px[0] += color.x;
       px[1] += color.y;
       px[2] += color.z;
-    }
-    if (wrote) {
-      A.paths.p0[i] = make_float4(ray.origin.x, ray.origin.y, ray.origin.z, ray.sdepth);
-      A.paths.p1[i] = make_float4(ray.direction.x, ray.direction.y, ray.direction.z,
-                                  ibits(pix | ((ray.isinside ? 1 : 0) << 31)));
-      A.paths.p2[i] = make_float4(color.x, color.y, color.z, ibits(bounces));
-      A.paths.pm[i] = matHit;
     }
     alive = COMPACT ? (bounces != 0) : true;
     key = matHit;

@@ -532,7 +532,7 @@ static void scatterRay(ray_t *ray, v3 intersect, v3 normal, const orc_material *
 /* KD traversals (src/pathtrace.cu:881-1020 and 1023-1235)               */
 /* ------------------------------------------------------------------ */
 typedef struct {
-    long long aabb, tri, hit;
+    long long aabb, tri, hit, leaves;
 } counters_t;
 
 typedef struct {
@@ -585,6 +585,7 @@ static void traverseKD(const orc_scene *s, ray_t ray, v3 *bary, hitrec_t *h, uns
         if (VIS(node->ID)) { currID = node->parentID; continue; }
         VIS(node->ID) = 1;
         int size = node->triIdSize;
+        if (size > 0) cnt->leaves++;
         if (size > 0) {
             int start = node->triIdStart, end = start + size;
             for (int i = start; i < end; i++) {
@@ -702,7 +703,7 @@ static void traceOneBounce(const orc_scene *s, const orc_opts *o, int depth, int
 #pragma omp parallel reduction(+ : ca, ct, ch)
     {
         unsigned char *visited = (unsigned char *)malloc((size_t)s->num_nodes + 1);
-        counters_t cnt = {0, 0, 0};
+        counters_t cnt = {0, 0, 0, 0};
 #pragma omp for schedule(dynamic, 256)
         for (int path_index = 0; path_index < num_paths; path_index++) {
             orc_path *P = &paths[path_index];
@@ -751,7 +752,7 @@ static void traceOneBounce(const orc_scene *s, const orc_opts *o, int depth, int
 
 int orc_trace_ray(const orc_scene *s, const float *origin, const float *direction, int hybrid, double *out) {
     unsigned char *visited = (unsigned char *)malloc((size_t)s->num_nodes + 1);
-    counters_t cnt = {0, 0, 0};
+    counters_t cnt = {0, 0, 0, 0};
     ray_t ray;
     ray.origin = V3(origin[0], origin[1], origin[2]);
     ray.direction = V3(direction[0], direction[1], direction[2]);
@@ -774,7 +775,7 @@ int orc_trace_ray(const orc_scene *s, const float *origin, const float *directio
     out[2] = h.intersect_point.x; out[3] = h.intersect_point.y; out[4] = h.intersect_point.z;
     out[5] = h.normal.x; out[6] = h.normal.y; out[7] = h.normal.z;
     out[8] = h.obj_intersect; out[9] = h.objMaterialIdx;
-    out[10] = (double)cnt.aabb; out[11] = (double)cnt.tri; out[12] = (double)cnt.hit;
+    out[10] = (double)cnt.aabb; out[11] = (double)cnt.tri; out[12] = (double)cnt.hit; out[13] = (double)cnt.leaves;
     free(visited);
     return 0;
 }
@@ -835,7 +836,7 @@ static int run_iteration(const orc_scene *s, const orc_opts *o, int iter, orc_pa
                           o->antialias);
     int depth = 0;
     int num_paths = pixelcount;
-    counters_t cnt = {0, 0, 0};
+    counters_t cnt = {0, 0, 0, 0};
     int complete = 0;
     int cap = o->bounce_cap > 0 ? o->bounce_cap : 8;
     st->bounces = 0;

@@ -207,7 +207,7 @@ int orc_paths_after(const orc_scene *s, const orc_opts *o, int iter, int stop_de
 
 /* One ray through the geoms + KD traversal of pathTraceOneBounceKDbare (no scatter).
  * out[0]=t_min out[1]=hit_geom_index out[2..4]=intersect point out[5..7]=normal
- * out[8]=obj_intersect out[9]=objMaterialIdx out[10..12]=aabb/tri/hit tests. */
+ * out[8]=obj_intersect out[9]=objMaterialIdx out[10..12]=aabb/tri/hit tests out[13]=leaves visited (size > 0). */
 int orc_trace_ray(const orc_scene *s, const float *origin, const float *direction, int hybrid, double *out);
 
 /* Device-math known answers shared with the HIP tests. */

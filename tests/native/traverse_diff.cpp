@@ -79,7 +79,7 @@ int main(int argc, char** argv) {
     f3 dd = normalize(mk3(tgt[0] - o[0], tgt[1] - o[1], tgt[2] - o[2]));
     if ((r % 7) == 0) dd = normalize(mk3(U(rng) - 0.5f, U(rng) - 0.5f, U(rng) - 0.5f));
     d[0] = dd.x; d[1] = dd.y; d[2] = dd.z;
-    double ref[13];
+    double ref[14];
     orc_trace_ray(&s, o, d, hybrid ? 1 : 0, ref);
     Ray ray;
     ray.origin = mk3(o[0], o[1], o[2]);
