@@ -314,11 +314,22 @@ struct WaveLeafLDS {
   int tbase[64];   // triangle index = tbase[owner] + pair index
   float4 od[64];   // ray origin.xyz, direction.x
   float2 dd[64];   // direction.y, direction.z
-  int lastPass[64];
+  unsigned long long lastPass[64];  // ((tri + 1) << 32) | bary.z bits, max
   int lastHit[64];
   int nhit[64];
   unsigned long long best[64];  // (t bits << 32) | triangle index, min
 };
+
+constexpr int BIG_LEAF = 64;  // leaves this size or larger are swept by the whole wave, one at a time
+
+__device__ inline unsigned long long wave_min_u64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(v, off);
+    v = o < v ? o : v;
+  }
+  return v;
+}
 
 __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -427,58 +438,114 @@ __device__ void traverseKD_wave(const DevScene& S, const Ray& ray, bool active, 
     }
     if (!__any(leaf)) break;
     // ---------------- leaf phase (wave-cooperative) ----------------
-    const int sz = leaf ? lsize : 0;
-    int incl = sz;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(incl, off);
-      if (lane >= off) incl += y;
-    }
-    const int P = __shfl(incl, 63);
-    W->pend[lane] = incl;
-    W->tbase[lane] = lstart - (incl - sz);
-    W->lastPass[lane] = -1;
-    W->lastHit[lane] = -1;
-    W->nhit[lane] = 0;
-    W->best[lane] = ~0ull;
-    wave_lds_sync();
-    for (int pi = lane; pi < P; pi += 64) {
-      int lo = 0, hi = 63;
-#pragma unroll
-      for (int st = 0; st < 6; st++) {
-        const int mid = (lo + hi) >> 1;
-        if (W->pend[mid] > pi) hi = mid; else lo = mid + 1;
+    // per lane results of this phase
+    int r_pass = 0;          // 0 = none, else tri + 1 of the last u/v pass
+    float r_bz = 0.0f;
+    int r_lasthit = -1, r_nhit = 0;
+    unsigned long long r_best = ~0ull;
+    // (a) big leaves: the whole wave sweeps one leaf at a time with a uniform ray
+    const bool big = leaf && lsize >= BIG_LEAF;
+    unsigned long long bigmask = __ballot(big);
+    while (bigmask) {
+      const int j = __builtin_ctzll(bigmask);
+      bigmask &= bigmask - 1;
+      const int jstart = __shfl(lstart, j), jsize = __shfl(lsize, j);
+      const f3 jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
+      const f3 jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
+      int u_pass = 0, u_lasthit = -1, u_nhit = 0;
+      float u_bz = 0.0f;
+      unsigned long long u_best = ~0ull;
+      for (int base = 0; base < jsize; base += 64) {
+        const int k = base + lane;
+        const int tri = jstart + k;
+        float bx = 0, by = 0, bzk = 0;
+        const int r = (k < jsize) ? tri_test(S, tri, jo, jd, bx, by, bzk) : 0;
+        const unsigned long long m1 = __ballot(r >= 1);
+        if (m1) {
+          const int last = 63 - __builtin_clzll(m1);
+          u_pass = jstart + base + last + 1;
+          u_bz = __shfl(bzk, last);
+          const unsigned long long m2 = __ballot(r == 2);
+          if (m2) {
+            u_lasthit = jstart + base + 63 - __builtin_clzll(m2);
+            u_nhit += __builtin_popcountll(m2);
+            unsigned long long key = ~0ull;
+            if (r == 2) {
+              f3 hp, nn;
+              const float t = tri_hit_t<HYBRID>(S, tri, jo, jd, bx, by, bzk, hp, nn);
+              if (t > 0.0f) key = ((unsigned long long)f2u(t) << 32) | (unsigned int)tri;
+            }
+            const unsigned long long wm = wave_min_u64(key);
+            u_best = wm < u_best ? wm : u_best;
+          }
+        }
       }
-      const int owner = lo;
-      const int tri = W->tbase[owner] + pi;
-      const float4 q0 = W->od[owner];
-      const float2 q1 = W->dd[owner];
-      const f3 oo = mk3(q0.x, q0.y, q0.z), dd = mk3(q0.w, q1.x, q1.y);
-      float bx, by, bzk;
-      const int r = tri_test(S, tri, oo, dd, bx, by, bzk);
-      if (r == 0) continue;
-      atomicMax(&W->lastPass[owner], tri);
-      if (r == 1) continue;
-      atomicMax(&W->lastHit[owner], tri);
-      atomicAdd(&W->nhit[owner], 1);
-      f3 hp, nn;
-      const float t = tri_hit_t<HYBRID>(S, tri, oo, dd, bx, by, bzk, hp, nn);
-      if (t > 0.0f) atomicMin(&W->best[owner], ((unsigned long long)f2u(t) << 32) | (unsigned int)tri);
+      if (lane == j) {
+        r_pass = u_pass;
+        r_bz = u_bz;
+        r_lasthit = u_lasthit;
+        r_nhit = u_nhit;
+        r_best = u_best;
+      }
     }
-    wave_lds_sync();
+    // (b) small leaves: all (ray, triangle) pairs spread over the 64 lanes
+    const int sz = (leaf && !big) ? lsize : 0;
+    if (__any(sz > 0)) {
+      int incl = sz;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const int y = __shfl_up(incl, off);
+        if (lane >= off) incl += y;
+      }
+      const int P = __shfl(incl, 63);
+      W->pend[lane] = incl;
+      W->tbase[lane] = lstart - (incl - sz);
+      W->lastPass[lane] = 0ull;
+      W->lastHit[lane] = -1;
+      W->nhit[lane] = 0;
+      W->best[lane] = ~0ull;
+      wave_lds_sync();
+      for (int pi = lane; pi < P; pi += 64) {
+        int lo = 0, hi = 63;
+#pragma unroll
+        for (int st = 0; st < 6; st++) {
+          const int mid = (lo + hi) >> 1;
+          if (W->pend[mid] > pi) hi = mid; else lo = mid + 1;
+        }
+        const int owner = lo;
+        const int tri = W->tbase[owner] + pi;
+        const float4 q0 = W->od[owner];
+        const float2 q1 = W->dd[owner];
+        const f3 oo = mk3(q0.x, q0.y, q0.z), dd = mk3(q0.w, q1.x, q1.y);
+        float bx, by, bzk;
+        const int r = tri_test(S, tri, oo, dd, bx, by, bzk);
+        if (r == 0) continue;
+        atomicMax(&W->lastPass[owner], ((unsigned long long)(unsigned int)(tri + 1) << 32) | f2u(bzk));
+        if (r == 1) continue;
+        atomicMax(&W->lastHit[owner], tri);
+        atomicAdd(&W->nhit[owner], 1);
+        f3 hp, nn;
+        const float t = tri_hit_t<HYBRID>(S, tri, oo, dd, bx, by, bzk, hp, nn);
+        if (t > 0.0f) atomicMin(&W->best[owner], ((unsigned long long)f2u(t) << 32) | (unsigned int)tri);
+      }
+      wave_lds_sync();
+      if (sz > 0) {
+        const unsigned long long lp = W->lastPass[lane];
+        r_pass = (int)(lp >> 32);
+        r_bz = u2f((uint32_t)(lp & 0xffffffffu));
+        r_lasthit = W->lastHit[lane];
+        r_nhit = W->nhit[lane];
+        r_best = W->best[lane];
+      }
+      wave_lds_sync();  // the LDS slots are rewritten by the next leaf phase
+    }
     if (leaf) {
       if (COUNT) cnt.tri += lsize;
-      const int lp = W->lastPass[lane];
-      if (lp >= 0) {
-        float bx, by, bzk;
-        tri_test(S, lp, o, d, bx, by, bzk);
-        bz = bzk;
-      }
-      const int nh = W->nhit[lane];
+      if (r_pass > 0) bz = r_bz;
+      const int nh = r_nhit;
       if (nh > 0) {
         if (COUNT) cnt.hit += nh;
-        const int lh = W->lastHit[lane];
-        h.objMaterialIdx = fbits(S.tv0[lh].w) + material_size - 1;
+        h.objMaterialIdx = fbits(S.tv0[r_lasthit].w) + material_size - 1;
         if (HYBRID) {
           for (int rep = 0; rep < (nh > 1 ? 2 : 1); rep++) {
             const bool parVis = (L == 0) ? sink
@@ -496,10 +563,9 @@ __device__ void traverseKD_wave(const DevScene& S, const Ray& ray, bool active, 
             }
           }
         }
-        const unsigned long long best = W->best[lane];
-        if (best != ~0ull) {
-          const float tb = u2f((uint32_t)(best >> 32));
-          const int k = (int)(uint32_t)(best & 0xffffffffu);
+        if (r_best != ~0ull) {
+          const float tb = u2f((uint32_t)(r_best >> 32));
+          const int k = (int)(uint32_t)(r_best & 0xffffffffu);
           if (h.t_min > tb) {
             float bx, by, bzk;
             tri_test(S, k, o, d, bx, by, bzk);
@@ -513,7 +579,6 @@ __device__ void traverseKD_wave(const DevScene& S, const Ray& ray, bool active, 
         }
       }
     }
-    wave_lds_sync();  // the LDS slots are rewritten by the next leaf phase
   }
 }
 #endif  // HIP
