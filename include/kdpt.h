@@ -187,6 +187,12 @@ int kdpt_debug_paths(kdpt_ctx *ctx, int iter, int stop_depth, kdpt_path_segment 
 /* Roofline counters: one extra, untimed iteration that also counts AABB tests, triangle
  * tests and triangle hits (aabb_tri_hit[3]); the image is not touched. */
 int kdpt_count_iteration(kdpt_ctx *ctx, int iter, unsigned long long *aabb_tri_hit);
+/* Diagnostic: cycle profile of the intersect kernel during the last kdpt_count_iteration.
+ * Copies up to n values -- node trips, node cycles, big-leaf sweeps, big-leaf cycles,
+ * small-leaf phases, small-leaf rounds, small-leaf cycles, recombination cycles, setup
+ * cycles, analytic-geometry cycles, post cycles, spare (each summed over 64-path chunks),
+ * chunks, chunk cycles, aabb, tri, hit -- and returns how many exist. */
+int kdpt_wave_profile(kdpt_ctx *ctx, unsigned long long *out, int n);
 /* Device-math known answers: sinf/cosf/pow-5 Fresnel/u01 evaluated by the gfx950 code. */
 int kdpt_selftest_math(const float *x, int n, float *sin_out, float *cos_out);
 int kdpt_selftest_rng(const int *iter_idx_depth, int n, int k, float *u_out);

@@ -59,10 +59,11 @@ struct DevScene {
   int has_obj;
   int num_nodes;
   int root;
-  // nodes: box0 = {minx,miny,minz,maxx}, box1 = {maxy,maxz,left,right}, meta = {parent,triStart,triSize,axis}
-  const float4* nbox0;
-  const float4* nbox1;
-  const int4* nmeta;
+  // nodes: 64-byte records [4*i .. 4*i+3] = {minx,miny,minz,maxx}, {maxy,maxz,left,right},
+  // {parent,triStart,triSize,axis}, padding; held as integer words (floats as their bits) so
+  // that no float move can canonicalise the -1 links
+  const int4* nodes;
+  const int4* pnodes;  // the same tree as 32-byte NodesPacked records, or null when ineligible
   // triangles: v0 (w = mtlIdx bits), e1 = v1-v0, e2 = v2-v0 (exactly glm's e1/e2)
   const float4* tv0;
   const float4* te1;
@@ -73,6 +74,8 @@ struct DevScene {
   const int* obj_material_offsets;
   // children of nodes[0] and nodes[1] for the hybrid skip line (-1 when absent)
   int n0_left, n0_right, n1_left, n1_right;
+  int trip_limit;  // bound on node steps per ray (a valid tree needs < 4 per node)
+  int* fault;      // set to 1 when a ray exceeds trip_limit (never for a validated tree)
 };
 
 struct Ray {
@@ -158,6 +161,21 @@ KDPT_HD bool intersectAABB(f3 o, f3 invdir, float4 b0, float4 b1, float& dist) {
   return true;
 }
 
+#if defined(__HIPCC__) || defined(__HIP__)
+// intersectAABB's decision (hit, and dist when hit) with IEEE min/max (v_min3/v_max3).
+// Equal to the std::min/max ternaries whenever no product is NaN -- i.e. whenever every
+// invdir component is finite -- because the results only feed comparisons (+-0 alike).
+__device__ inline bool intersectAABB_fast(f3 o, f3 invdir, float4 b0, float4 b1, float& dist) {
+  const float v1 = (b0.x - o.x) * invdir.x, v2 = (b0.w - o.x) * invdir.x;
+  const float v3 = (b0.y - o.y) * invdir.y, v4 = (b1.x - o.y) * invdir.y;
+  const float v5 = (b0.z - o.z) * invdir.z, v6 = (b1.y - o.z) * invdir.z;
+  const float dmin = fmaxf(fmaxf(fminf(v1, v2), fminf(v3, v4)), fminf(v5, v6));
+  const float dmax = fminf(fminf(fmaxf(v1, v2), fmaxf(v3, v4)), fmaxf(v5, v6));
+  dist = dmin;
+  return !(dmax < 0.0f) && !(dmin > dmax);
+}
+#endif
+
 struct Hit {
   float t_min;
   int hit_geom_index;
@@ -186,20 +204,22 @@ KDPT_HD void traverseKD(const DevScene& S, const Ray& ray, Hit& h, int material_
   float bz = FLT_MAXV;  // bary.z
   while (true) {
     if (cur == -1) break;
-    const float4 b0 = S.nbox0[cur];
-    const float4 b1 = S.nbox1[cur];
-    const int4 meta = S.nmeta[cur];
-    const int left = fbits(b1.z), right = fbits(b1.w), parent = meta.x;
+    const int4 q0 = S.nodes[4 * cur];
+    const int4 q1 = S.nodes[4 * cur + 1];
+    const int4 meta = S.nodes[4 * cur + 2];
+    const float4 b0 = make_float4(ibits(q0.x), ibits(q0.y), ibits(q0.z), ibits(q0.w));
+    const float4 b1 = make_float4(ibits(q1.x), ibits(q1.y), 0.0f, 0.0f);
+    const int left = q1.z, right = q1.w, parent = meta.x;
     const int lvlbit = (L > 0) ? (2 * (L - 1) + (int)((ps >> (L - 1)) & 1u)) : 0;
     const bool curVis = (L == 0) ? rootv : (((cb >> lvlbit) & 1u) != 0u);
-    if (!hitGeom && parent == -1 && curVis) break;
+    if (!hitGeom && cur == S.root && curVis) break;
     hitGeom = intersectAABB(o, invdir, b0, b1, dist);
     if (COUNT) cnt.aabb++;
     bool up = false;
     if (curVis) {
       up = true;
     } else {
-      if (!hitGeom && parent == -1) break;
+      if (!hitGeom && cur == S.root) break;
       if (!hitGeom || dist > bz) up = true;
     }
     if (up) {
@@ -309,6 +329,68 @@ KDPT_HD void traverseKD(const DevScene& S, const Ray& ray, Hit& h, int material_
 //   hit record    = FIRST triangle reaching the minimum t with t > 0 && t_min > t
 //   skip marks    = applied min(#intersected, 2) times (idempotent from the 2nd on)
 // ---------------------------------------------------------------------------
+// ---------------------------------------------------------------------------
+// Node sources.  The traversal reads one node per step; where it reads it from
+// is a template parameter:
+//   NodesWide   : 64-byte records in HBM (any tree the validator accepts)
+//   NodesPacked : 32-byte records (4 per 128-byte line), in HBM or -- when the
+//                 kernel has copied the tree there -- in LDS.  Packing:
+//     w0..w5 = min.xyz, max.xyz (float bits)
+//     w6     = left | right << 16 (0xffff = -1), or triStart for a leaf with triangles
+//     w7     = parent (16 bits, 0xffff = -1) | axis << 16 | hasTris << 18 | triSize << 19
+//   eligible when num_nodes < 65535, axis in 0..2, and every node with triangles
+//   is childless with triSize < 8192 (checked on the host, else NodesWide).
+// ---------------------------------------------------------------------------
+struct NodeRec {
+  float4 b0;     // min.xyz, max.x
+  float4 b1;     // max.y, max.z, -, -
+  int left, right, parent, axis, triStart, triSize;
+};
+
+struct NodesWide {
+  const int4* p;
+  __device__ NodeRec operator()(int i) const {
+    const int4 q0 = p[4 * i], q1 = p[4 * i + 1], q2 = p[4 * i + 2];
+    NodeRec r;
+    r.b0 = make_float4(ibits(q0.x), ibits(q0.y), ibits(q0.z), ibits(q0.w));
+    r.b1 = make_float4(ibits(q1.x), ibits(q1.y), 0.0f, 0.0f);
+    r.left = q1.z;
+    r.right = q1.w;
+    r.parent = q2.x;
+    r.triStart = q2.y;
+    r.triSize = q2.z;
+    r.axis = q2.w;
+    return r;
+  }
+};
+
+__device__ inline int link16(uint32_t v) { return v == 0xffffu ? -1 : (int)v; }
+
+struct NodesPacked {
+  const int4* p;  // global or LDS (address space inferred after inlining)
+  __device__ NodeRec operator()(int i) const {
+    const int4 q0 = p[2 * i], q1 = p[2 * i + 1];
+    NodeRec r;
+    r.b0 = make_float4(ibits(q0.x), ibits(q0.y), ibits(q0.z), ibits(q0.w));
+    r.b1 = make_float4(ibits(q1.x), ibits(q1.y), 0.0f, 0.0f);
+    const uint32_t w6 = (uint32_t)q1.z, w7 = (uint32_t)q1.w;
+    const bool tris = (w7 >> 18) & 1u;
+    r.left = tris ? -1 : link16(w6 & 0xffffu);
+    r.right = tris ? -1 : link16(w6 >> 16);
+    r.parent = link16(w7 & 0xffffu);
+    r.axis = (int)((w7 >> 16) & 3u);
+    r.triStart = (int)w6;
+    r.triSize = tris ? (int)(w7 >> 19) : 0;
+    return r;
+  }
+};
+
+// wave-profile slots (count mode): trips / cycles of each part of the intersect kernel
+enum ProfSlot {
+  PROF_NODE_TRIPS, PROF_NODE_CYC, PROF_BIG_SWEEPS, PROF_BIG_CYC, PROF_SMALL_PHASES, PROF_SMALL_ROUNDS,
+  PROF_SMALL_CYC, PROF_FINAL_CYC, PROF_SETUP_CYC, PROF_GEOM_CYC, PROF_POST_CYC, PROF_SPARE, PROF_SLOTS
+};
+
 struct WaveLeafLDS {
   int pend[64];    // inclusive end of each lane's pair range
   int tbase[64];   // triangle index = tbase[owner] + pair index
@@ -318,7 +400,21 @@ struct WaveLeafLDS {
   int lastHit[64];
   int nhit[64];
   unsigned long long best[64];  // (t bits << 32) | triangle index, min
+  // count mode only, kept by lane 0 (slots: PROF_* below); last timestamp
+  unsigned long long prof[12];
+  unsigned long long tlast;
 };
+
+__device__ inline void prof_add(WaveLeafLDS* W, int k, unsigned long long v) {
+  if ((threadIdx.x & 63) == 0) W->prof[k] += v;
+}
+__device__ inline void prof_lap(WaveLeafLDS* W, int k) {  // cycles since the last lap into prof[k]
+  const unsigned long long now = __builtin_readcyclecounter();
+  if ((threadIdx.x & 63) == 0) {
+    if (k >= 0) W->prof[k] += now - W->tlast;
+    W->tlast = now;
+  }
+}
 
 constexpr int BIG_LEAF = 64;  // leaves this size or larger are swept by the whole wave, one at a time
 
@@ -339,10 +435,19 @@ __device__ inline void wave_lds_sync() {
 
 // glm::intersectRayTriangle on (o, d) and triangle i; returns 0 = miss before the u/v
 // tests passed, 1 = passed u/v but t < 0 (bary.z still written), 2 = intersected.
+struct TriData {
+  float4 v0, e1, e2;
+};
+__device__ inline TriData tri_load(const DevScene& S, int i) { return TriData{S.tv0[i], S.te1[i], S.te2[i]}; }
+
+__device__ inline int tri_test_v(const TriData& T, f3 o, f3 d, float& bx, float& by, float& bz);
+
 __device__ inline int tri_test(const DevScene& S, int i, f3 o, f3 d, float& bx, float& by, float& bz) {
-  const float4 tv = S.tv0[i];
-  const float4 e1v = S.te1[i];
-  const float4 e2v = S.te2[i];
+  return tri_test_v(tri_load(S, i), o, d, bx, by, bz);
+}
+
+__device__ inline int tri_test_v(const TriData& T, f3 o, f3 d, float& bx, float& by, float& bz) {
+  const float4 tv = T.v0, e1v = T.e1, e2v = T.e2;
   const f3 v0 = mk3(tv.x, tv.y, tv.z), e1 = mk3(e1v.x, e1v.y, e1v.z), e2 = mk3(e2v.x, e2v.y, e2v.z);
   const f3 p = cross(d, e2);
   const float a = dot(e1, p);
@@ -371,9 +476,10 @@ __device__ inline float tri_hit_t(const DevScene& S, int i, f3 o, f3 d, float bx
   return distance(o, hit);
 }
 
-template <bool HYBRID, bool COUNT>
-__device__ void traverseKD_wave(const DevScene& S, const Ray& ray, bool active, Hit& h, int material_size,
-                                TraverseCounters& cnt, WaveLeafLDS* W) {
+template <bool HYBRID, bool COUNT, typename NodeSrc>
+__device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const Ray& ray, bool active, Hit& h,
+                               int material_size, TraverseCounters& cnt, WaveLeafLDS* W) {
+  int objTri = -1;  // returned: the triangle whose hit record won (valid when h.obj_intersect)
   const int lane = threadIdx.x & 63;
   const f3 o = ray.origin, d = ray.direction;
   W->od[lane] = make_float4(o.x, o.y, o.z, d.x);
@@ -384,59 +490,94 @@ __device__ void traverseKD_wave(const DevScene& S, const Ray& ray, bool active, 
   bool rootv = false, sink = false, hitGeom = false;
   bool done = !active;
   float dist = -1.0f, bz = FLT_MAXV;
+  int guard = 0;  // node steps of this ray; > S.trip_limit means a corrupt tree: stop and flag
+  int phases = 0;  // leaf phases of this wave, bounded the same way
+  bool fault = false;
+  // IEEE min/max AABB slabs are exact unless some invdir component is infinite (wave-uniform)
+  const bool fastAABB = __all(!active || (fabsf(invdir.x) < FLT_INFV && fabsf(invdir.y) < FLT_INFV &&
+                                          fabsf(invdir.z) < FLT_INFV));
   while (true) {
     // ---------------- node phase ----------------
     bool leaf = false;
     int lstart = 0, lsize = 0;
     bool lfirst = true;
-    while (!done && !leaf) {
-      if (cur == -1) { done = true; break; }
-      const float4 b0 = S.nbox0[cur];
-      const float4 b1 = S.nbox1[cur];
-      const int4 meta = S.nmeta[cur];
-      const int left = fbits(b1.z), right = fbits(b1.w), parent = meta.x;
-      const int lvlbit = (L > 0) ? (2 * (L - 1) + (int)((ps >> (L - 1)) & 1u)) : 0;
-      const bool curVis = (L == 0) ? rootv : (((cb >> lvlbit) & 1u) != 0u);
-      if (!hitGeom && parent == -1 && curVis) { done = true; break; }
-      hitGeom = intersectAABB(o, invdir, b0, b1, dist);
-      if (COUNT) cnt.aabb++;
-      bool up = curVis;
-      if (!curVis) {
-        if (!hitGeom && parent == -1) { done = true; break; }
-        up = (!hitGeom || dist > bz);
-      }
-      if (up) {
-        if (L == 0) rootv = true; else cb |= 1u << lvlbit;
-        if (left == -1) sink = true; else cb |= 1u << (2 * L);
-        if (right == -1) sink = true; else cb |= 1u << (2 * L + 1);
-        cur = parent;
-        L--;
-        continue;
-      }
-      const bool leftFirst = HYBRID ? (comp(d, meta.w) > 0.0f) : true;
+    int trips = 0;
+    if (COUNT) prof_lap(W, -1);
+    // One trip = one step of the reference's loop for every lane still walking nodes.  The
+    // body runs for the whole wave and commits by selects on `walk`, and the per-lane flags
+    // live in one register, so a trip carries no exec-mask bookkeeping.  Exact for a
+    // validated tree (only the root has parentID == -1): at the root `up` ends the walk (the
+    // reference exits before or after its test, or climbs to -1), so hitGeom only feeds the
+    // AABB count.
+    enum : uint32_t { F_ROOTV = 1, F_SINK = 2, F_HITGEOM = 4, F_DONE = 8, F_LEAF = 16, F_LFIRST = 32, F_FAULT = 64 };
+    uint32_t fl = (rootv ? F_ROOTV : 0u) | (sink ? F_SINK : 0u) | (hitGeom ? F_HITGEOM : 0u) | (done ? F_DONE : 0u) |
+                  F_LFIRST;
+    while (true) {
+      const bool walk = (fl & (F_DONE | F_LEAF)) == 0u;
+      if (!__any(walk)) break;
+      if (COUNT) trips += walk ? 1 : 0;
+      const NodeRec nd = nodes(cur < 0 ? 0 : cur);
+      const int left = nd.left, right = nd.right;
+      const uint32_t Lu = (uint32_t)L;
+      const uint32_t vb = (2u * Lu - 2u + ((ps >> ((Lu - 1u) & 31u)) & 1u)) & 31u;  // own flag (L > 0)
+      const bool curVis = (L == 0) ? ((fl & F_ROOTV) != 0u) : (((cb >> vb) & 1u) != 0u);
+      const bool isRoot = cur == S.root;
+      float dd;
+      const bool hg = fastAABB ? intersectAABB_fast(o, invdir, nd.b0, nd.b1, dd)
+                               : intersectAABB(o, invdir, nd.b0, nd.b1, dd);
+      if (COUNT && walk && !(isRoot && curVis && !(fl & F_HITGEOM))) cnt.aabb++;
+      const bool up = curVis || !hg || dd > bz;
+      const bool leftFirst = HYBRID ? (comp(d, nd.axis) > 0.0f) : true;
       const uint32_t fside = leftFirst ? 0u : 1u;
+      const uint32_t cl = (cb >> ((2u * Lu) & 31u)) & 3u;  // child flags of this level
       const int first = leftFirst ? left : right, second = leftFirst ? right : left;
-      int next = -1;
-      uint32_t nside = 0;
-      if (first != -1 && !((cb >> (2 * L + fside)) & 1u)) { next = first; nside = fside; }
-      else if (second != -1 && !((cb >> (2 * L + (fside ^ 1u))) & 1u)) { next = second; nside = fside ^ 1u; }
-      if (next != -1) {
-        ps = (ps & ~(1u << L)) | (nside << L);
-        cb &= ~(3u << (2u * (uint32_t)(L + 1)));
-        if (L == 0 && nside == 0u) cb |= g << 2;
-        L++;
-        cur = next;
-        continue;
-      }
-      if (L == 0) rootv = true; else cb |= 1u << lvlbit;
-      if (meta.z > 0) {
-        leaf = true;
-        lstart = meta.y;
-        lsize = meta.z;
-        lfirst = leftFirst;
+      const bool takeFirst = first != -1 && !((cl >> fside) & 1u);
+      const bool takeSecond = second != -1 && !((cl >> (fside ^ 1u)) & 1u);
+      const bool descend = !up && (takeFirst || takeSecond);
+      const uint32_t nside = takeFirst ? fside : (fside ^ 1u);
+      // nodeIDs[ID] = true unless descending; nodeIDs[left] = nodeIDs[right] = true when climbing
+      uint32_t ncb = cb | ((!descend && L > 0) ? (1u << vb) : 0u);
+      ncb |= up ? ((left != -1 ? 1u : 0u) | (right != -1 ? 2u : 0u)) << ((2u * Lu) & 31u) : 0u;
+      const uint32_t dcb = (ncb & ~(3u << ((2u * Lu + 2u) & 31u))) | ((L == 0 && nside == 0u) ? (g << 2) : 0u);
+      const bool runaway = guard >= S.trip_limit;
+      const bool lf = !up && !descend && nd.triSize > 0;
+      uint32_t nfl = fl & ~(F_HITGEOM | F_LFIRST);
+      nfl |= (!descend && L == 0) ? F_ROOTV : 0u;
+      nfl |= (up && (left == -1 || right == -1)) ? F_SINK : 0u;
+      nfl |= hg ? F_HITGEOM : 0u;
+      nfl |= ((isRoot && up) || runaway) ? F_DONE : 0u;
+      nfl |= runaway ? F_FAULT : 0u;
+      nfl |= lf ? F_LEAF : 0u;
+      nfl |= leftFirst ? F_LFIRST : 0u;
+      if (walk) {  // commit (selects)
+        cb = descend ? dcb : ncb;
+        ps = descend ? ((ps & ~(1u << (Lu & 31u))) | (nside << (Lu & 31u))) : ps;
+        cur = up ? nd.parent : (descend ? (takeFirst ? first : second) : cur);
+        L += descend ? 1 : (up ? -1 : 0);
+        guard++;
+        fl = nfl;
+        lstart = nd.triStart;
+        lsize = nd.triSize;
       }
     }
+    rootv = (fl & F_ROOTV) != 0u;
+    sink = (fl & F_SINK) != 0u;
+    hitGeom = (fl & F_HITGEOM) != 0u;
+    done = (fl & F_DONE) != 0u;
+    leaf = (fl & F_LEAF) != 0u;
+    lfirst = (fl & F_LFIRST) != 0u;
+    fault = fault || (fl & F_FAULT) != 0u;
+    if (COUNT) {
+      prof_lap(W, PROF_NODE_CYC);
+      for (int off = 32; off > 0; off >>= 1) trips = max(trips, __shfl_xor(trips, off));
+      prof_add(W, PROF_NODE_TRIPS, (unsigned long long)trips);  // wave-level trips = the slowest lane's
+    }
+    if (__any(fault) && lane == 0) atomicOr(S.fault, 1);
     if (!__any(leaf)) break;
+    if (++phases > S.trip_limit) {  // uniform; unreachable for a validated tree
+      if (lane == 0) atomicOr(S.fault, 2);
+      break;
+    }
     // ---------------- leaf phase (wave-cooperative) ----------------
     // per lane results of this phase
     int r_pass = 0;          // 0 = none, else tri + 1 of the last u/v pass
@@ -446,51 +587,88 @@ __device__ void traverseKD_wave(const DevScene& S, const Ray& ray, bool active, 
     // (a) big leaves: the whole wave sweeps one leaf at a time with a uniform ray
     const bool big = leaf && lsize >= BIG_LEAF;
     unsigned long long bigmask = __ballot(big);
-    while (bigmask) {
-      const int j = __builtin_ctzll(bigmask);
+    if (bigmask) {
+      // Sweeps of 64 triangles over every big leaf of the wave in turn, the next sweep's
+      // triangles loaded while the current one is tested.
+      int j = __builtin_ctzll(bigmask);
       bigmask &= bigmask - 1;
-      const int jstart = __shfl(lstart, j), jsize = __shfl(lsize, j);
-      const f3 jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
-      const f3 jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
+      int jstart = __shfl(lstart, j), jsize = __shfl(lsize, j);
+      f3 jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
+      f3 jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
+      int base = 0;
+      TriData nxt = tri_load(S, jstart + min(lane, jsize - 1));
       int u_pass = 0, u_lasthit = -1, u_nhit = 0;
       float u_bz = 0.0f;
       unsigned long long u_best = ~0ull;
-      for (int base = 0; base < jsize; base += 64) {
-        const int k = base + lane;
-        const int tri = jstart + k;
+      while (true) {
+        if (COUNT) prof_add(W, PROF_BIG_SWEEPS, 1);
+        const TriData cur_t = nxt;
+        const int cj = j, cstart = jstart, cbase = base;
+        const bool cin = base + lane < jsize;
+        const f3 co = jo, cd = jd;
+        // advance to the next sweep (this leaf or the next big leaf) and start its loads
+        base += 64;
+        bool more = true, leaf_end = false;
+        if (base >= jsize) {
+          leaf_end = true;
+          if (bigmask) {
+            j = __builtin_ctzll(bigmask);
+            bigmask &= bigmask - 1;
+            jstart = __shfl(lstart, j);
+            jsize = __shfl(lsize, j);
+            jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
+            jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
+            base = 0;
+          } else {
+            more = false;
+          }
+        }
+        if (more) nxt = tri_load(S, jstart + min(base + lane, jsize - 1));
+        // test the current sweep
+        const int tri = cstart + cbase + lane;
         float bx = 0, by = 0, bzk = 0;
-        const int r = (k < jsize) ? tri_test(S, tri, jo, jd, bx, by, bzk) : 0;
+        const int r = cin ? tri_test_v(cur_t, co, cd, bx, by, bzk) : 0;
         const unsigned long long m1 = __ballot(r >= 1);
         if (m1) {
           const int last = 63 - __builtin_clzll(m1);
-          u_pass = jstart + base + last + 1;
+          u_pass = cstart + cbase + last + 1;
           u_bz = __shfl(bzk, last);
           const unsigned long long m2 = __ballot(r == 2);
           if (m2) {
-            u_lasthit = jstart + base + 63 - __builtin_clzll(m2);
+            u_lasthit = cstart + cbase + 63 - __builtin_clzll(m2);
             u_nhit += __builtin_popcountll(m2);
             unsigned long long key = ~0ull;
             if (r == 2) {
               f3 hp, nn;
-              const float t = tri_hit_t<HYBRID>(S, tri, jo, jd, bx, by, bzk, hp, nn);
+              const float t = tri_hit_t<HYBRID>(S, tri, co, cd, bx, by, bzk, hp, nn);
               if (t > 0.0f) key = ((unsigned long long)f2u(t) << 32) | (unsigned int)tri;
             }
             const unsigned long long wm = wave_min_u64(key);
             u_best = wm < u_best ? wm : u_best;
           }
         }
-      }
-      if (lane == j) {
-        r_pass = u_pass;
-        r_bz = u_bz;
-        r_lasthit = u_lasthit;
-        r_nhit = u_nhit;
-        r_best = u_best;
+        if (leaf_end) {
+          if (lane == cj) {
+            r_pass = u_pass;
+            r_bz = u_bz;
+            r_lasthit = u_lasthit;
+            r_nhit = u_nhit;
+            r_best = u_best;
+          }
+          u_pass = 0;
+          u_lasthit = -1;
+          u_nhit = 0;
+          u_bz = 0.0f;
+          u_best = ~0ull;
+        }
+        if (!more) break;
       }
     }
+    if (COUNT) prof_lap(W, PROF_BIG_CYC);
     // (b) small leaves: all (ray, triangle) pairs spread over the 64 lanes
     const int sz = (leaf && !big) ? lsize : 0;
     if (__any(sz > 0)) {
+      if (COUNT) prof_add(W, PROF_SMALL_PHASES, 1);
       int incl = sz;
 #pragma unroll
       for (int off = 1; off < 64; off <<= 1) {
@@ -505,28 +683,49 @@ __device__ void traverseKD_wave(const DevScene& S, const Ray& ray, bool active, 
       W->nhit[lane] = 0;
       W->best[lane] = ~0ull;
       wave_lds_sync();
-      for (int pi = lane; pi < P; pi += 64) {
+      if (COUNT) prof_add(W, PROF_SMALL_ROUNDS, (unsigned long long)((P + 63) / 64));
+      // pair pi -> owner lane (binary search over the inclusive ends) and triangle; the next
+      // round's pair is located and its triangle loaded while the current one is tested
+      auto owner_of = [&](int q) {
         int lo = 0, hi = 63;
 #pragma unroll
         for (int st = 0; st < 6; st++) {
           const int mid = (lo + hi) >> 1;
-          if (W->pend[mid] > pi) hi = mid; else lo = mid + 1;
+          if (W->pend[mid] > q) hi = mid; else lo = mid + 1;
         }
-        const int owner = lo;
-        const int tri = W->tbase[owner] + pi;
-        const float4 q0 = W->od[owner];
-        const float2 q1 = W->dd[owner];
+        return lo;
+      };
+      int pi = lane;
+      int owner = 0, tri = 0;
+      TriData nxt{};
+      if (pi < P) {
+        owner = owner_of(pi);
+        tri = W->tbase[owner] + pi;
+        nxt = tri_load(S, tri);
+      }
+      while (pi < P) {
+        const TriData cur_t = nxt;
+        const int cowner = owner, ctri = tri;
+        pi += 64;
+        if (pi < P) {
+          owner = owner_of(pi);
+          tri = W->tbase[owner] + pi;
+          nxt = tri_load(S, tri);
+        }
+        const float4 q0 = W->od[cowner];
+        const float2 q1 = W->dd[cowner];
         const f3 oo = mk3(q0.x, q0.y, q0.z), dd = mk3(q0.w, q1.x, q1.y);
         float bx, by, bzk;
-        const int r = tri_test(S, tri, oo, dd, bx, by, bzk);
-        if (r == 0) continue;
-        atomicMax(&W->lastPass[owner], ((unsigned long long)(unsigned int)(tri + 1) << 32) | f2u(bzk));
-        if (r == 1) continue;
-        atomicMax(&W->lastHit[owner], tri);
-        atomicAdd(&W->nhit[owner], 1);
-        f3 hp, nn;
-        const float t = tri_hit_t<HYBRID>(S, tri, oo, dd, bx, by, bzk, hp, nn);
-        if (t > 0.0f) atomicMin(&W->best[owner], ((unsigned long long)f2u(t) << 32) | (unsigned int)tri);
+        const int r = tri_test_v(cur_t, oo, dd, bx, by, bzk);
+        if (r >= 1)
+          atomicMax(&W->lastPass[cowner], ((unsigned long long)(unsigned int)(ctri + 1) << 32) | f2u(bzk));
+        if (r == 2) {
+          atomicMax(&W->lastHit[cowner], ctri);
+          atomicAdd(&W->nhit[cowner], 1);
+          f3 hp, nn;
+          const float t = tri_hit_t<HYBRID>(S, ctri, oo, dd, bx, by, bzk, hp, nn);
+          if (t > 0.0f) atomicMin(&W->best[cowner], ((unsigned long long)f2u(t) << 32) | (unsigned int)ctri);
+        }
       }
       wave_lds_sync();
       if (sz > 0) {
@@ -539,6 +738,7 @@ __device__ void traverseKD_wave(const DevScene& S, const Ray& ray, bool active, 
       }
       wave_lds_sync();  // the LDS slots are rewritten by the next leaf phase
     }
+    if (COUNT) prof_lap(W, PROF_SMALL_CYC);
     if (leaf) {
       if (COUNT) cnt.tri += lsize;
       if (r_pass > 0) bz = r_bz;
@@ -566,20 +766,18 @@ __device__ void traverseKD_wave(const DevScene& S, const Ray& ray, bool active, 
         if (r_best != ~0ull) {
           const float tb = u2f((uint32_t)(r_best >> 32));
           const int k = (int)(uint32_t)(r_best & 0xffffffffu);
-          if (h.t_min > tb) {
-            float bx, by, bzk;
-            tri_test(S, k, o, d, bx, by, bzk);
-            f3 hp, nn;
-            h.t_min = tri_hit_t<HYBRID>(S, k, o, d, bx, by, bzk, hp, nn);
+          if (h.t_min > tb) {  // tb is tri_hit_t's value for triangle k (the winner's point and
+            h.t_min = tb;        // normal are recomputed from k by the shading kernel)
             h.hit_geom_index = S.obj_material_offsets[fbits(S.tv0[k].w)];
-            h.ip = hp;
-            h.normal = nn;
             h.obj_intersect = true;
+            objTri = k;
           }
         }
       }
     }
+    if (COUNT) prof_lap(W, PROF_FINAL_CYC);
   }
+  return objTri;
 }
 #endif  // HIP
 

@@ -21,6 +21,8 @@
 // host-only builds (tests/native differential harness): HIP's vector types
 struct float4 { float x, y, z, w; };
 struct int4 { int x, y, z, w; };
+static inline int4 make_int4(int x, int y, int z, int w) { return int4{x, y, z, w}; }
+static inline float4 make_float4(float x, float y, float z, float w) { return float4{x, y, z, w}; }
 #endif
 
 namespace kdpt {
@@ -31,6 +33,7 @@ constexpr float TWO_PI_F = 6.2831853071795864769252867665590057683943f;
 constexpr float SQRT_OF_ONE_THIRD_F = 0.5773502691896257645091487805019574556476f;
 constexpr float FLT_EPS = 1.19209290e-07f;   // std::numeric_limits<float>::epsilon()
 constexpr float FLT_MAXV = 3.40282347e+38f;
+constexpr float FLT_INFV = __builtin_inff();
 
 struct f3 {
   float x, y, z;

@@ -2,9 +2,11 @@
 // reference's per-sample hot path (src/pathtrace.cu:2405-2635 `pathtrace`).
 //
 // One iteration = k_gen_rays, then per bounce (cap 8, src/pathtrace.cu:2608):
-//   k_bounce   : intersect (6 analytic geoms + KD traversal) + scatterRay +
-//                shadeMaterial + partialGather fused, one lane per live path;
-//                writes the updated path in place and the tile's survivor count
+//   k_trace    : the intersect kernel -- 6 analytic geoms + KD traversal, one lane
+//                per live path, persistent waves pulling 64-path chunks, the KD
+//                tree read from LDS when it fits (32-byte packed nodes)
+//   k_shade    : scatterRay + shadeMaterial + partialGather, writes the path in
+//                place and the tile's survivor count
 //   k_scan     : exclusive scan of tile counts (key-major when iter == 2 sorts)
 //   k_scatter  : stable compaction (thrust::remove_if) -- and on iter 2 the
 //                stable sort by materialIdHit (thrust::sort, a merge sort) --
@@ -15,6 +17,7 @@
 
 #include <algorithm>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -57,6 +60,7 @@ struct PathBuf {
 
 struct Counters {
   unsigned long long aabb, tri, hit;
+  unsigned long long wave[PROF_SLOTS + 2];  // WaveLeafLDS::prof summed over chunks, then chunks, cycles
 };
 
 __device__ inline unsigned int lane_prefix(unsigned long long mask) {
@@ -68,12 +72,13 @@ __device__ inline unsigned int lane_prefix(unsigned long long mask) {
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int traceDepth, PathBuf out,
                                                   float focalLength, float dofAngle, int antialias, int* counts,
-                                                  int ncounts) {
+                                                  int ncounts, int* work, int nwork) {
   const int W = cam.resolution[0], H = cam.resolution[1];
   const int index = blockIdx.x * blockDim.x + threadIdx.x;
   if (index == 0) {
     counts[0] = W * H;
     for (int k = 1; k < ncounts; k++) counts[k] = 0;
+    for (int k = 0; k < nwork; k++) work[k] = 0;
   }
   if (index >= W * H) return;
   const int x = index % W, y = index / W;
@@ -118,11 +123,148 @@ __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int
 }
 
 // ---------------------------------------------------------------------------
-// pathTraceOneBounceKDbare + shadeMaterial + partialGather (fused)
+// pathTraceOneBounceKDbare (src/pathtrace.cu:1489-1662): the intersect kernel.
+//
+// Persistent: one 1024-thread workgroup per CU slot; every wave repeatedly takes
+// the next 64 live paths from a device counter, so a wave that drew heavy rays
+// never holds a CU idle.  With MODE == TREE_LDS the workgroup first copies the
+// packed KD tree into LDS and every node step is an LDS read.
+// Output per path: hit code (-1 none, g >= 0 analytic geom g, -(k + 2) triangle k)
+// and objMaterialIdx; k_shade recomputes the winner's point and normal with the
+// same functions, so nothing else needs to travel.
 // ---------------------------------------------------------------------------
-struct BounceArgs {
+enum TreeMode { TREE_WIDE = 0, TREE_PACKED = 1, TREE_LDS = 2 };
+constexpr int TRACE_BLOCK = 1024;
+
+struct TraceArgs {
   DevScene S;
   PathBuf paths;
+  int2* hits;
+  const int* counts;
+  int* work;  // [cap] chunk counters, zeroed by k_gen_rays
+  int depth;
+  Counters* counters;
+};
+
+__device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, WaveLeafLDS* W,
+                                      unsigned long long t_k0) {
+  unsigned int a = cnt.aabb, tr = cnt.tri, hi = cnt.hit;
+  for (int off = 32; off > 0; off >>= 1) {
+    a += __shfl_down(a, off);
+    tr += __shfl_down(tr, off);
+    hi += __shfl_down(hi, off);
+  }
+  if ((threadIdx.x & 63) == 0) {
+    atomicAdd(&C->aabb, (unsigned long long)a);
+    atomicAdd(&C->tri, (unsigned long long)tr);
+    atomicAdd(&C->hit, (unsigned long long)hi);
+    for (int k = 0; k < PROF_SLOTS; k++) {
+      atomicAdd(&C->wave[k], W->prof[k]);
+      W->prof[k] = 0;
+    }
+    atomicAdd(&C->wave[PROF_SLOTS], 1ull);
+    atomicAdd(&C->wave[PROF_SLOTS + 1], __builtin_readcyclecounter() - t_k0);
+  }
+}
+
+template <bool HYBRID, bool COUNT, int MODE>
+__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
+  extern __shared__ int4 s_tree[];
+  __shared__ WaveLeafLDS s_leaf[TRACE_BLOCK / 64];
+  const DevScene& S = A.S;
+  const int n = A.counts[A.depth];
+  if (MODE == TREE_LDS) {
+    if (n == 0) return;  // uniform: nothing to trace
+    const int words = 2 * S.num_nodes;
+    for (int k = threadIdx.x; k < words; k += TRACE_BLOCK) s_tree[k] = S.pnodes[k];
+    __syncthreads();
+  }
+  const int lane = threadIdx.x & 63;
+  WaveLeafLDS* W = &s_leaf[threadIdx.x >> 6];
+  if (COUNT && lane < PROF_SLOTS) W->prof[lane] = 0;
+  int* work = A.work + A.depth;
+  // First chunk: the wave's own index (no atomic -- thousands of waves start at once);
+  // later chunks from the shared counter, which starts past the statically taken ones.
+  const int nwaves = gridDim.x * (TRACE_BLOCK / 64);
+  int chunk = blockIdx.x * (TRACE_BLOCK / 64) + (threadIdx.x >> 6);
+  while (true) {
+    if (__ballot(1) != ~0ull) {  // the chunk protocol needs the whole wave here
+      atomicOr(S.fault, 4);
+      break;
+    }
+    if (chunk * 64 >= n) break;  // uniform
+    const unsigned long long t_k0 = COUNT ? __builtin_readcyclecounter() : 0ull;
+    if (COUNT) prof_lap(W, -1);
+    const int i = chunk * 64 + lane;
+    const bool valid = i < n;
+    float4 q0 = make_float4(0, 0, 0, 0), q1 = make_float4(0, 0, 1, 0);
+    int bounces = 0;
+    if (valid) {
+      q0 = A.paths.p0[i];
+      q1 = A.paths.p1[i];
+      bounces = fbits(A.paths.p2[i].w);
+    }
+    Ray ray;
+    ray.origin = mk3(q0.x, q0.y, q0.z);
+    ray.direction = mk3(q1.x, q1.y, q1.z);
+    ray.isinside = false;
+    ray.sdepth = q0.w;
+    const bool active = valid && bounces > 0;
+    Hit h;
+    h.t_min = FLT_MAXV;
+    h.hit_geom_index = -1;
+    h.obj_intersect = false;
+    h.objMaterialIdx = -1;
+    h.ip = mk3(0, 0, 0);
+    h.normal = mk3(0, 0, 0);
+    if (COUNT) prof_lap(W, PROF_SETUP_CYC);
+    if (active) {
+      f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
+      float t = 0;
+      for (int g = 0; g < S.num_geoms; g++) {
+        const DevGeom& G = S.geoms[g];
+        if (G.type == 1) t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
+        else if (G.type == 0) t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+        if (t > 0.0f && h.t_min > t) {
+          h.t_min = t;
+          h.hit_geom_index = g;
+        }
+      }
+    }
+    if (COUNT) prof_lap(W, PROF_GEOM_CYC);
+    TraverseCounters cnt{};
+    int objTri = -1;
+    if (S.has_obj && S.num_nodes > 0) {  // uniform: every lane of the wave takes part
+      if (MODE == TREE_LDS)
+        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesPacked{s_tree}, ray, active, h, S.num_materials, cnt, W);
+      else if (MODE == TREE_PACKED)
+        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ray, active, h, S.num_materials, cnt, W);
+      else
+        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesWide{S.nodes}, ray, active, h, S.num_materials, cnt, W);
+    }
+    if (valid && active) {
+      const int code = h.hit_geom_index == -1 ? -1 : (h.obj_intersect ? -(objTri + 2) : h.hit_geom_index);
+      A.hits[i] = make_int2(code, h.objMaterialIdx);
+    }
+    if (COUNT) {
+      prof_lap(W, PROF_POST_CYC);
+      flush_counters(A.counters, cnt, W, t_k0);
+    }
+    int next = 0;
+    if (lane == 0) next = nwaves + atomicAdd(work, 1);
+    chunk = __shfl(next, 0);
+  }
+}
+
+// ---------------------------------------------------------------------------
+// shadeMaterial + scatterRay (src/pathtrace.cu:1885-2100, src/interactions.h) +
+// partialGather, one lane per live path; writes the path in place and the tile's
+// survivor count (or, when sorting, its per-material histogram).
+// ---------------------------------------------------------------------------
+struct ShadeArgs {
+  DevScene S;
+  PathBuf paths;
+  const int2* hits;
   float* image;
   const int* counts;
   int depth;
@@ -132,84 +274,59 @@ struct BounceArgs {
   int* tile_counts;  // [ntiles] or key-major [MAX_KEYS][ntiles] when sorting
   int ntiles;
   int nkeys;
-  Counters* counters;
-  unsigned long long* total_segments;  // running sum of paths launched into this kernel
+  unsigned long long* total_segments;  // running sum of paths launched into the intersect kernel
 };
 
-template <bool HYBRID, bool COMPACT, bool SORT, bool COUNT>
-__global__ __launch_bounds__(TILE) void k_bounce(BounceArgs A) {
+template <bool HYBRID, bool COMPACT, bool SORT>
+__global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   const int n = A.counts[A.depth];
   const int tile = blockIdx.x;
   if (tile * TILE >= n) return;  // uniform per block
   const int i = tile * TILE + threadIdx.x;
   if (i == 0) atomicAdd(A.total_segments, (unsigned long long)n);
   __shared__ int s_hist[MAX_KEYS];
-  __shared__ unsigned int s_cnt[3];
   if (SORT) {
     for (int k = threadIdx.x; k < MAX_KEYS; k += TILE) s_hist[k] = 0;
+    __syncthreads();
   }
-  if (COUNT && threadIdx.x < 3) s_cnt[threadIdx.x] = 0;
-  if (SORT || COUNT) __syncthreads();
-  __shared__ WaveLeafLDS s_leaf[TILE / 64];
+  const DevScene& S = A.S;
   bool alive = false;
   int key = 0;
-  TraverseCounters cnt{0, 0, 0};
-  const bool valid = i < n;
-  float4 q0 = make_float4(0, 0, 0, 0), q1 = make_float4(0, 0, 0, 0), q2 = make_float4(0, 0, 0, 0);
-  int matHit = 0;
-  if (valid) {
-    q0 = A.paths.p0[i];
-    q1 = A.paths.p1[i];
-    q2 = A.paths.p2[i];
-    matHit = A.paths.pm[i];
-  }
-  const int pw = fbits(q1.w);
-  const int pix = pw & 0x7fffffff;
-  Ray ray;
-  ray.origin = mk3(q0.x, q0.y, q0.z);
-  ray.direction = mk3(q1.x, q1.y, q1.z);
-  ray.isinside = (pw >> 31) & 1;
-  ray.sdepth = q0.w;
-  f3 color = mk3(q2.x, q2.y, q2.z);
-  int bounces = fbits(q2.w);
-  const bool active = valid && bounces > 0;
-  const DevScene& S = A.S;
-  Hit h;
-  h.t_min = FLT_MAXV;
-  h.hit_geom_index = -1;
-  h.obj_intersect = false;
-  h.objMaterialIdx = -1;
-  h.ip = mk3(0, 0, 0);
-  h.normal = mk3(0, 0, 0);
-  if (active) {
-    f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
-    float t = 0;
-    for (int g = 0; g < S.num_geoms; g++) {
-      const DevGeom& G = S.geoms[g];
-      if (G.type == 1) t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
-      else if (G.type == 0) t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
-      if (t > 0.0f && h.t_min > t) {
-        h.t_min = t;
-        h.hit_geom_index = g;
-        h.ip = tmp_i;
-        h.normal = tmp_n;
-      }
-    }
-  }
-  if (S.has_obj && S.num_nodes > 0)  // uniform: every lane of the wave takes part
-    traverseKD_wave<HYBRID, COUNT>(S, ray, active, h, S.num_materials, cnt, &s_leaf[threadIdx.x >> 6]);
-  if (valid) {
-    if (active) {
-      float isect_t;
+  if (i < n) {
+    const float4 q0 = A.paths.p0[i], q1 = A.paths.p1[i], q2 = A.paths.p2[i];
+    int matHit = A.paths.pm[i];
+    const int pw = fbits(q1.w);
+    const int pix = pw & 0x7fffffff;
+    Ray ray;
+    ray.origin = mk3(q0.x, q0.y, q0.z);
+    ray.direction = mk3(q1.x, q1.y, q1.z);
+    ray.isinside = (pw >> 31) & 1;
+    ray.sdepth = q0.w;
+    f3 color = mk3(q2.x, q2.y, q2.z);
+    int bounces = fbits(q2.w);
+    if (bounces > 0) {
+      const int2 hr = A.hits[i];
+      float isect_t = -1.0f;
       int isect_mat = 0;
-      if (h.hit_geom_index == -1) {
-        isect_t = -1.0f;
-      } else {
+      if (hr.x != -1) {
+        f3 ip, nrm;
+        float t;
+        int mid;
+        if (hr.x < -1) {  // triangle: the traversal's final recomputation, repeated
+          const int k = -hr.x - 2;
+          float bx, by, bzk;
+          tri_test(S, k, ray.origin, ray.direction, bx, by, bzk);
+          t = tri_hit_t<HYBRID>(S, k, ray.origin, ray.direction, bx, by, bzk, ip, nrm);
+          mid = hr.y;
+        } else {
+          const DevGeom& G = S.geoms[hr.x];
+          t = G.type == 1 ? boxIntersectionTest(G, ray, ip, nrm) : sphereIntersectionTest(G, ray, ip, nrm);
+          mid = G.materialid;
+        }
         Rng rng = seeded_rng(A.iter, i, A.depth);
-        const int mid = h.obj_intersect ? h.objMaterialIdx : S.geoms[h.hit_geom_index].materialid;
         matHit = mid;
-        scatterRay(ray, h.ip, h.normal, S.materials[mid], rng, A.softness);
-        isect_t = h.t_min;
+        scatterRay(ray, ip, nrm, S.materials[mid], rng, A.softness);
+        isect_t = t;
         isect_mat = mid;
       }
       shade(isect_t, isect_mat, S.materials, A.enable_sss != 0, ray, color, bounces);
@@ -229,20 +346,6 @@ __global__ __launch_bounds__(TILE) void k_bounce(BounceArgs A) {
     alive = COMPACT ? (bounces != 0) : true;
     key = matHit;
   }
-  if (COUNT) {
-    // wave-reduce then one LDS atomic per wave
-    unsigned int a = cnt.aabb, tr = cnt.tri, hi = cnt.hit;
-    for (int off = 32; off > 0; off >>= 1) {
-      a += __shfl_down(a, off);
-      tr += __shfl_down(tr, off);
-      hi += __shfl_down(hi, off);
-    }
-    if ((threadIdx.x & 63) == 0) {
-      atomicAdd(&s_cnt[0], a);
-      atomicAdd(&s_cnt[1], tr);
-      atomicAdd(&s_cnt[2], hi);
-    }
-  }
   if (SORT) {
     if (alive) atomicAdd(&s_hist[key], 1);
     __syncthreads();
@@ -250,14 +353,6 @@ __global__ __launch_bounds__(TILE) void k_bounce(BounceArgs A) {
   } else {
     const int c = __syncthreads_count(alive);
     if (threadIdx.x == 0) A.tile_counts[tile] = c;
-  }
-  if (COUNT) {
-    __syncthreads();
-    if (threadIdx.x == 0) {
-      atomicAdd(&A.counters->aabb, (unsigned long long)s_cnt[0]);
-      atomicAdd(&A.counters->tri, (unsigned long long)s_cnt[1]);
-      atomicAdd(&A.counters->hit, (unsigned long long)s_cnt[2]);
-    }
   }
 }
 
@@ -438,16 +533,23 @@ struct kdpt_ctx {
   int cur = 0;
   float* image = nullptr;
   bool image_external = false;
-  int* counts = nullptr;  // [cap + 2]
+  int* counts = nullptr;  // [cap + 2] live paths per bounce, [cap + 2] fault flag, then [cap] work counters
+  int* work = nullptr;
+  int2* hits = nullptr;   // [npix] hit code + objMaterialIdx from the intersect kernel
+  int tree_mode = 0;      // TreeMode
+  int trace_grid = 0;     // persistent intersect workgroups
+  size_t tree_lds = 0;    // dynamic LDS bytes of the intersect kernel (TREE_LDS)
   int* tile_counts = nullptr;
   int* tile_off = nullptr;
   Counters* counters = nullptr;
+  Counters last_profile{};
   unsigned long long* total_segments = nullptr;  // device running total (async use)
   int* h_counts = nullptr;  // pinned
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> bounce_ev;
   kdpt_stats stats{};
   bool count_mode = false;
+  bool sync_debug = false;  // KDPT_SYNC_DEBUG=1: synchronise and log after every launch
 };
 
 namespace {
@@ -470,6 +572,88 @@ int dupload(kdpt_ctx* c, T** p, const T* src, size_t n) {
 }
 
 int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count);
+
+// NodesPacked records (kdpt_device.h); false when the tree does not fit the format.
+bool pack_nodes(const kdpt_node_bare* N, int nn, std::vector<int4>& out) {
+  if (nn >= 0xffff) return false;
+  out.assign(2 * (size_t)nn, make_int4(0, 0, 0, 0));
+  auto l16 = [](int v) { return v == -1 ? 0xffffu : (uint32_t)v; };
+  for (int i = 0; i < nn; i++) {
+    const kdpt_node_bare& n = N[i];
+    const bool tris = n.triIdSize > 0;
+    if (tris && (n.leftID != -1 || n.rightID != -1 || n.triIdSize >= (1 << 13))) return false;
+    const uint32_t axis = n.axis == 0 ? 0u : (n.axis == 1 ? 1u : 2u);  // comp(): anything else reads z
+    const uint32_t w6 = tris ? (uint32_t)n.triIdStart : (l16(n.leftID) | (l16(n.rightID) << 16));
+    const uint32_t w7 = l16(n.parentID) | (axis << 16) | ((tris ? 1u : 0u) << 18) |
+                        ((tris ? (uint32_t)n.triIdSize : 0u) << 19);
+    out[2 * i] = make_int4(fbits(n.mins[0]), fbits(n.mins[1]), fbits(n.mins[2]), fbits(n.maxs[0]));
+    out[2 * i + 1] = make_int4(fbits(n.maxs[1]), fbits(n.maxs[2]), (int)w6, (int)w7);
+  }
+  return true;
+}
+
+template <bool HYBRID, bool COUNT, int MODE>
+int trace_occupancy(kdpt_ctx* c, size_t lds, int* blocks) {
+  if (lds > 0)
+    HIP_TRY(hipFuncSetAttribute((const void*)k_trace<HYBRID, COUNT, MODE>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace<HYBRID, COUNT, MODE>, TRACE_BLOCK, lds));
+  return KDPT_OK;
+}
+
+// Pick where the intersect kernel reads the tree from, and its persistent grid.
+int setup_trace(kdpt_ctx* c) {
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, c->device));
+  c->tree_mode = c->S.pnodes ? TREE_PACKED : TREE_WIDE;
+  c->tree_lds = 0;
+  const size_t static_lds = sizeof(WaveLeafLDS) * (TRACE_BLOCK / 64);
+  const size_t tree_bytes = 32 * (size_t)c->S.num_nodes;
+  const size_t lds_max = prop.sharedMemPerBlock > 0 ? prop.sharedMemPerBlock : 65536;
+  if (c->S.pnodes && static_lds + tree_bytes <= lds_max) {
+    c->tree_mode = TREE_LDS;
+    c->tree_lds = tree_bytes;
+  }
+  int blocks = 0;
+  int rc = KDPT_OK;
+  for (int hyb = 0; hyb < 2 && !rc; hyb++)
+    for (int cnt = 0; cnt < 2 && !rc; cnt++) {
+      int b = 0;
+      if (c->tree_mode == TREE_LDS)
+        rc = hyb ? (cnt ? trace_occupancy<true, true, TREE_LDS>(c, c->tree_lds, &b)
+                        : trace_occupancy<true, false, TREE_LDS>(c, c->tree_lds, &b))
+                 : (cnt ? trace_occupancy<false, true, TREE_LDS>(c, c->tree_lds, &b)
+                        : trace_occupancy<false, false, TREE_LDS>(c, c->tree_lds, &b));
+      else if (c->tree_mode == TREE_PACKED)
+        rc = hyb ? (cnt ? trace_occupancy<true, true, TREE_PACKED>(c, 0, &b)
+                        : trace_occupancy<true, false, TREE_PACKED>(c, 0, &b))
+                 : (cnt ? trace_occupancy<false, true, TREE_PACKED>(c, 0, &b)
+                        : trace_occupancy<false, false, TREE_PACKED>(c, 0, &b));
+      else
+        rc = hyb ? (cnt ? trace_occupancy<true, true, TREE_WIDE>(c, 0, &b)
+                        : trace_occupancy<true, false, TREE_WIDE>(c, 0, &b))
+                 : (cnt ? trace_occupancy<false, true, TREE_WIDE>(c, 0, &b)
+                        : trace_occupancy<false, false, TREE_WIDE>(c, 0, &b));
+      if (!rc && (blocks == 0 || b < blocks)) blocks = b;
+    }
+  if (rc) return rc;
+  if (blocks < 1) return fail(KDPT_ERR_UNSUPPORTED, "intersect kernel does not fit on a CU");
+  c->trace_grid = blocks * prop.multiProcessorCount;
+  return KDPT_OK;
+}
+
+// A ray that needs more node steps than any valid tree allows sets the fault word and stops;
+// the iteration then reports an error instead of returning a silently wrong image.
+int fault_error(kdpt_ctx* c, int code) {
+  (void)hipMemset(c->counts + c->cap + 2, 0, sizeof(int));
+  return fail(KDPT_ERR_HIP, "KD traversal exceeded its step bound (inconsistent tree), code " + std::to_string(code));
+}
+
+int check_fault(kdpt_ctx* c) {
+  int f = 0;
+  HIP_TRY(hipMemcpy(&f, c->counts + c->cap + 2, sizeof(int), hipMemcpyDeviceToHost));
+  return f ? fault_error(c, f) : KDPT_OK;
+}
 
 }  // namespace
 
@@ -530,6 +714,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     if (sc->num_nodes > 1 && N[0].leftID != 1) return fail(KDPT_ERR_UNSUPPORTED, "node 1 must be root's left child");
     level.assign(sc->num_nodes, 0);
     for (int i = 1; i < sc->num_nodes; i++) {
+      // only the root has no parent (the traversal tests `parentID == -1` as `cur == root`)
+      if (N[i].parentID < 0 || N[i].parentID >= i) return fail(KDPT_ERR_ARG, "inconsistent KD parent links");
       level[i] = level[N[i].parentID] + 1;
       if (level[i] > 15) return fail(KDPT_ERR_UNSUPPORTED, "KD tree deeper than 15 levels");
     }
@@ -599,13 +785,14 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   c->S.n0_left = c->S.n0_right = c->S.n1_left = c->S.n1_right = -1;
   if (sc->has_obj && sc->num_nodes > 0) {
     const int nn = sc->num_nodes, nt = sc->num_tris;
-    std::vector<float4> b0(nn), b1(nn), tv(nt), e1(nt), e2(nt), n0(nt), n1(nt), n2(nt);
-    std::vector<int4> meta(nn);
-    for (int i = 0; i < nn; i++) {
+    std::vector<int4> nodes(4 * (size_t)nn);
+    std::vector<float4> tv(nt), e1(nt), e2(nt), n0(nt), n1(nt), n2(nt);
+    for (int i = 0; i < nn; i++) {  // one 64-byte record per node (one cache line per visit)
       const kdpt_node_bare& N = sc->nodes[i];
-      b0[i] = make_float4(N.mins[0], N.mins[1], N.mins[2], N.maxs[0]);
-      b1[i] = make_float4(N.maxs[1], N.maxs[2], ibits(N.leftID), ibits(N.rightID));
-      meta[i] = make_int4(N.parentID, N.triIdStart, N.triIdSize, N.axis);
+      nodes[4 * i + 0] = make_int4(fbits(N.mins[0]), fbits(N.mins[1]), fbits(N.mins[2]), fbits(N.maxs[0]));
+      nodes[4 * i + 1] = make_int4(fbits(N.maxs[1]), fbits(N.maxs[2]), N.leftID, N.rightID);
+      nodes[4 * i + 2] = make_int4(N.parentID, N.triIdStart, N.triIdSize, N.axis);
+      nodes[4 * i + 3] = make_int4(0, 0, 0, 0);
     }
     for (int i = 0; i < nt; i++) {
       const kdpt_tri_bare& T = sc->tris[i];
@@ -617,19 +804,23 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
       n1[i] = make_float4(T.nx2, T.ny2, T.nz2, 0.0f);
       n2[i] = make_float4(T.nx3, T.ny3, T.nz3, 0.0f);
     }
-    float4 *db0, *db1, *dtv, *de1, *de2, *dn0, *dn1, *dn2;
-    int4* dmeta;
+    int4* dnodes;
+    float4 *dtv, *de1, *de2, *dn0, *dn1, *dn2;
     int* doff;
-    if ((rc = dupload(c, &db0, b0.data(), nn)) || (rc = dupload(c, &db1, b1.data(), nn)) ||
-        (rc = dupload(c, &dmeta, meta.data(), nn)) || (rc = dupload(c, &dtv, tv.data(), nt)) ||
+    if ((rc = dupload(c, &dnodes, nodes.data(), nodes.size())) || (rc = dupload(c, &dtv, tv.data(), nt)) ||
         (rc = dupload(c, &de1, e1.data(), nt)) || (rc = dupload(c, &de2, e2.data(), nt)) ||
         (rc = dupload(c, &dn0, n0.data(), nt)) || (rc = dupload(c, &dn1, n1.data(), nt)) ||
         (rc = dupload(c, &dn2, n2.data(), nt)) ||
         (rc = dupload(c, &doff, sc->obj_materialOffsets, (size_t)sc->num_shapes)))
       return bail(rc);
-    c->S.nbox0 = db0;
-    c->S.nbox1 = db1;
-    c->S.nmeta = dmeta;
+    c->S.nodes = dnodes;
+    c->S.pnodes = nullptr;
+    std::vector<int4> packed;
+    if (pack_nodes(sc->nodes, nn, packed)) {
+      int4* dp;
+      if ((rc = dupload(c, &dp, packed.data(), packed.size()))) return bail(rc);
+      c->S.pnodes = dp;
+    }
     c->S.tv0 = dtv;
     c->S.te1 = de1;
     c->S.te2 = de2;
@@ -658,12 +849,22 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   } else if ((rc = dalloc(c, &c->image, 3 * (size_t)c->npix))) {
     return bail(rc);
   }
-  if ((rc = dalloc(c, &c->counts, c->cap + 2)) || (rc = dalloc(c, &c->tile_counts, (size_t)MAX_KEYS * c->ntiles)) ||
+  // counts[0..cap+1]: live paths per bounce (rewritten every iteration); counts[cap+2]: fault flag
+  if ((rc = dalloc(c, &c->counts, 2 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) || (rc = dalloc(c, &c->tile_counts, (size_t)MAX_KEYS * c->ntiles)) ||
       (rc = dalloc(c, &c->tile_off, (size_t)MAX_KEYS * c->ntiles)) || (rc = dalloc(c, &c->counters, 1)) ||
       (rc = dalloc(c, &c->total_segments, 1)))
     return bail(rc);
-  if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 2), hipHostMallocDefault) != hipSuccess)
+  if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 3), hipHostMallocDefault) != hipSuccess)
     return bail(fail(KDPT_ERR_HIP, "hipHostMalloc"));
+  if (hipMemset(c->counts, 0, sizeof(int) * (2 * c->cap + 3)) != hipSuccess) return bail(fail(KDPT_ERR_HIP, "memset"));
+  c->S.fault = c->counts + c->cap + 2;
+  c->work = c->counts + c->cap + 3;
+  {
+    const char* e = getenv("KDPT_SYNC_DEBUG");
+    c->sync_debug = e && e[0] == '1';
+  }
+  if ((rc = setup_trace(c))) return bail(rc);
+  c->S.trip_limit = 8 * std::max(c->S.num_nodes, 1) + 64;
   if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
     return bail(fail(KDPT_ERR_HIP, "hipEventCreate"));
   c->bounce_ev.resize(2 * (size_t)c->cap);
@@ -693,7 +894,7 @@ int kdpt_trace_iteration_async(kdpt_ctx* c, int frame, int iter) {
 int kdpt_synchronize(kdpt_ctx* c) {
   if (!c) return fail(KDPT_ERR_ARG, "null ctx");
   HIP_TRY(hipStreamSynchronize(c->stream));
-  return KDPT_OK;
+  return check_fault(c);
 }
 
 int kdpt_trace_iteration(kdpt_ctx* c, int frame, int iter) {
@@ -704,8 +905,9 @@ int kdpt_trace_iteration(kdpt_ctx* c, int frame, int iter) {
   int rc = launch_iteration(c, iter, -1, c->count_mode);
   if (rc) return rc;
   HIP_TRY(hipEventRecord(c->ev1, c->stream));
-  HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts, sizeof(int) * (c->cap + 1), hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts, sizeof(int) * (c->cap + 3), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if (c->h_counts[c->cap + 2]) return fault_error(c, c->h_counts[c->cap + 2]);
   float ms = 0;
   HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->stats.ms_last_iteration = ms;
@@ -810,6 +1012,7 @@ int kdpt_debug_paths(kdpt_ctx* c, int iter, int stop_depth, kdpt_path_segment* o
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts, sizeof(int) * (c->cap + 2), hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  if ((rc = check_fault(c))) { (void)hipFree(d); (void)hipFree(scratch); return rc; }
   const int n = c->h_counts[depth_slot];
   *npaths = n;
   HIP_TRY(hipMemcpy(out, d, sizeof(kdpt_path_segment) * (size_t)n, hipMemcpyDeviceToHost));
@@ -839,13 +1042,26 @@ int kdpt_count_iteration(kdpt_ctx* c, int iter, unsigned long long* aabb_tri_hit
   if (!rc) {
     HIP_TRY(hipMemcpyAsync(&h, c->counters, sizeof h, hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    rc = check_fault(c);
   }
   (void)hipFree(scratch);
   (void)hipFree(scratch_tot);
   aabb_tri_hit[0] = h.aabb;
   aabb_tri_hit[1] = h.tri;
   aabb_tri_hit[2] = h.hit;
+  c->last_profile = h;
   return rc;
+}
+
+int kdpt_wave_profile(kdpt_ctx* c, unsigned long long* out, int n) {
+  if (!c || !out) return fail(KDPT_ERR_ARG, "null arg");
+  unsigned long long v[PROF_SLOTS + 5];
+  for (int k = 0; k < PROF_SLOTS + 2; k++) v[k] = c->last_profile.wave[k];
+  v[PROF_SLOTS + 2] = c->last_profile.aabb;
+  v[PROF_SLOTS + 3] = c->last_profile.tri;
+  v[PROF_SLOTS + 4] = c->last_profile.hit;
+  for (int k = 0; k < n && k < PROF_SLOTS + 5; k++) out[k] = v[k];
+  return PROF_SLOTS + 5;
 }
 
 int kdpt_selftest_math(const float* x, int n, float* so, float* co) {
@@ -892,12 +1108,33 @@ int kdpt_selftest_fresnel(const float* cs, int n, float ior, float* f) {
 
 namespace {
 
-template <bool HYBRID, bool COMPACT, bool SORT>
-void launch_bounce(kdpt_ctx* c, const BounceArgs& a, bool count) {
-  if (count)
-    hipLaunchKernelGGL((k_bounce<HYBRID, COMPACT, SORT, true>), dim3(c->ntiles), dim3(TILE), 0, c->stream, a);
+template <bool HYBRID, bool COUNT>
+void launch_trace_mode(kdpt_ctx* c, const TraceArgs& a) {
+  const dim3 g(c->trace_grid), b(TRACE_BLOCK);
+  if (c->tree_mode == TREE_LDS)
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS>), g, b, c->tree_lds, c->stream, a);
+  else if (c->tree_mode == TREE_PACKED)
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_PACKED>), g, b, 0, c->stream, a);
   else
-    hipLaunchKernelGGL((k_bounce<HYBRID, COMPACT, SORT, false>), dim3(c->ntiles), dim3(TILE), 0, c->stream, a);
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_WIDE>), g, b, 0, c->stream, a);
+}
+
+void launch_trace(kdpt_ctx* c, const TraceArgs& a, bool count) {
+  const bool hyb = c->opt.short_stack != 0;
+  if (hyb) { if (count) launch_trace_mode<true, true>(c, a); else launch_trace_mode<true, false>(c, a); }
+  else { if (count) launch_trace_mode<false, true>(c, a); else launch_trace_mode<false, false>(c, a); }
+}
+
+template <bool HYBRID>
+void launch_shade_h(kdpt_ctx* c, const ShadeArgs& a, bool compact, bool sort) {
+  const dim3 g(c->ntiles), b(TILE);
+  if (compact) {
+    if (sort) hipLaunchKernelGGL((k_shade<HYBRID, true, true>), g, b, 0, c->stream, a);
+    else hipLaunchKernelGGL((k_shade<HYBRID, true, false>), g, b, 0, c->stream, a);
+  } else {
+    if (sort) hipLaunchKernelGGL((k_shade<HYBRID, false, true>), g, b, 0, c->stream, a);
+    else hipLaunchKernelGGL((k_shade<HYBRID, false, false>), g, b, 0, c->stream, a);
+  }
 }
 
 int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
@@ -905,14 +1142,33 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
   c->cur = 0;
   hipLaunchKernelGGL(k_gen_rays, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->cam, gen_iter,
                      c->traceDepth, c->buf[0], c->opt.focal_length, c->opt.dof_angle, c->opt.antialias, c->counts,
-                     c->cap + 2);
+                     c->cap + 2, c->work, c->cap);
   HIP_TRY(hipGetLastError());
   const bool compact = c->opt.compaction != 0;
   const bool sort = (iter == 2);
   for (int depth = 0; depth < c->cap; depth++) {
-    BounceArgs a;
+    TraceArgs t;
+    t.S = c->S;
+    t.paths = c->buf[c->cur];
+    t.hits = c->hits;
+    t.counts = c->counts;
+    t.work = c->work;
+    t.depth = depth;
+    t.counters = c->counters;
+    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(c->bounce_ev[2 * depth], c->stream));
+    launch_trace(c, t, count);
+    HIP_TRY(hipGetLastError());
+    if (c->sync_debug) {
+      fprintf(stderr, "[kdpt] trace depth %d launched (grid %d, mode %d, lds %zu)\n", depth, c->trace_grid,
+              c->tree_mode, c->tree_lds);
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      fprintf(stderr, "[kdpt] trace depth %d done\n", depth);
+    }
+    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(c->bounce_ev[2 * depth + 1], c->stream));
+    ShadeArgs a;
     a.S = c->S;
     a.paths = c->buf[c->cur];
+    a.hits = c->hits;
     a.image = c->image;
     a.counts = c->counts;
     a.depth = depth;
@@ -922,19 +1178,14 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
     a.tile_counts = c->tile_counts;
     a.ntiles = c->ntiles;
     a.nkeys = c->nkeys;
-    a.counters = c->counters;
     a.total_segments = c->total_segments;
-    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(c->bounce_ev[2 * depth], c->stream));
-    const bool hyb = c->opt.short_stack != 0;
-    if (hyb) {
-      if (compact) { if (sort) launch_bounce<true, true, true>(c, a, count); else launch_bounce<true, true, false>(c, a, count); }
-      else { if (sort) launch_bounce<true, false, true>(c, a, count); else launch_bounce<true, false, false>(c, a, count); }
-    } else {
-      if (compact) { if (sort) launch_bounce<false, true, true>(c, a, count); else launch_bounce<false, true, false>(c, a, count); }
-      else { if (sort) launch_bounce<false, false, true>(c, a, count); else launch_bounce<false, false, false>(c, a, count); }
-    }
+    if (c->opt.short_stack) launch_shade_h<true>(c, a, compact, sort);
+    else launch_shade_h<false>(c, a, compact, sort);
     HIP_TRY(hipGetLastError());
-    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(c->bounce_ev[2 * depth + 1], c->stream));
+    if (c->sync_debug) {
+      HIP_TRY(hipStreamSynchronize(c->stream));
+      fprintf(stderr, "[kdpt] shade depth %d done\n", depth);
+    }
     if (compact || sort) {
       hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, c->stream, c->tile_counts, c->tile_off, c->counts, depth,
                          c->ntiles, sort ? c->nkeys : 1);

@@ -19,7 +19,7 @@ from typing import Optional
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libkdpt.so")
+LIB_PATH = os.environ.get("KDPT_LIBRARY") or os.path.join(HERE, "libkdpt.so")
 
 KDPT_OK = 0
 
@@ -102,7 +102,7 @@ assert C.sizeof(NodeBare) == 64 and C.sizeof(TriBare) == 76 and C.sizeof(PathSeg
 EXPORTS = [
     "kdpt_default_options", "kdpt_create", "kdpt_trace_iteration", "kdpt_trace_iteration_async", "kdpt_synchronize",
     "kdpt_read_image", "kdpt_write_pbo", "kdpt_reset", "kdpt_get_stats", "kdpt_destroy", "kdpt_last_error",
-    "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_selftest_math", "kdpt_selftest_rng",
+    "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_wave_profile", "kdpt_selftest_math", "kdpt_selftest_rng",
     "kdpt_selftest_fresnel", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
 ]
 
@@ -138,6 +138,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_image_device_ptr.argtypes = [C.c_void_p, P(C.c_void_p)]
     lib.kdpt_debug_paths.argtypes = [C.c_void_p, C.c_int, C.c_int, P(PathSegment), P(C.c_int)]
     lib.kdpt_count_iteration.argtypes = [C.c_void_p, C.c_int, P(C.c_ulonglong)]
+    lib.kdpt_wave_profile.argtypes = [C.c_void_p, P(C.c_ulonglong), C.c_int]
     lib.kdpt_selftest_math.argtypes = [P(C.c_float), C.c_int, P(C.c_float), P(C.c_float)]
     lib.kdpt_selftest_rng.argtypes = [P(C.c_int), C.c_int, C.c_int, P(C.c_float)]
     lib.kdpt_selftest_fresnel.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
@@ -355,6 +356,16 @@ class PathTracer:
         out = (C.c_ulonglong * 3)()
         _check(self.lib.kdpt_count_iteration(self._ctx, int(iteration), out), "kdpt_count_iteration")
         return int(out[0]), int(out[1]), int(out[2])
+
+    def wave_profile(self):
+        """Cycle profile of the intersect kernel in the last count_iteration (kdpt_wave_profile)."""
+        out = (C.c_ulonglong * 64)()
+        n = self.lib.kdpt_wave_profile(self._ctx, out, 64)
+        _check(0 if n > 0 else n, "kdpt_wave_profile")
+        keys = ("node_trips", "node_cycles", "big_sweeps", "big_cycles", "small_phases", "small_rounds",
+                "small_cycles", "final_cycles", "setup_cycles", "geom_cycles", "post_cycles", "spare",
+                "chunks", "chunk_cycles", "aabb", "tri", "hit")
+        return dict(zip(keys, (int(out[k]) for k in range(n))))
 
     def close(self):
         if self._ctx:

@@ -24,13 +24,14 @@ int main(int argc, char** argv) {
   const unsigned seed = (unsigned)atoi(argv[4]);
   const bool hybrid = atoi(argv[5]) != 0;
   const int nn = s.num_nodes, nt = s.num_tris;
-  std::vector<float4> b0(nn), b1(nn), tv(nt), e1(nt), e2(nt), n0(nt), n1(nt), n2(nt);
-  std::vector<int4> meta(nn);
+  std::vector<int4> nodes(4 * (size_t)nn);
+  std::vector<float4> tv(nt), e1(nt), e2(nt), n0(nt), n1(nt), n2(nt);
   for (int i = 0; i < nn; i++) {
     const orc_node& N = s.nodes[i];
-    b0[i] = float4{N.mins[0], N.mins[1], N.mins[2], N.maxs[0]};
-    b1[i] = float4{N.maxs[1], N.maxs[2], ibits(N.leftID), ibits(N.rightID)};
-    meta[i] = int4{N.parentID, N.triIdStart, N.triIdSize, N.axis};
+    nodes[4 * i] = int4{fbits(N.mins[0]), fbits(N.mins[1]), fbits(N.mins[2]), fbits(N.maxs[0])};
+    nodes[4 * i + 1] = int4{fbits(N.maxs[1]), fbits(N.maxs[2]), N.leftID, N.rightID};
+    nodes[4 * i + 2] = int4{N.parentID, N.triIdStart, N.triIdSize, N.axis};
+    nodes[4 * i + 3] = int4{0, 0, 0, 0};
   }
   for (int i = 0; i < nt; i++) {
     const orc_tri& T = s.tris[i];
@@ -56,7 +57,7 @@ int main(int argc, char** argv) {
   S.has_obj = s.has_obj;
   S.num_nodes = nn;
   S.root = 0;
-  S.nbox0 = b0.data(); S.nbox1 = b1.data(); S.nmeta = meta.data();
+  S.nodes = nodes.data();
   S.tv0 = tv.data(); S.te1 = e1.data(); S.te2 = e2.data();
   S.tn0 = n0.data(); S.tn1 = n1.data(); S.tn2 = n2.data();
   S.obj_material_offsets = s.obj_materialOffsets;
