@@ -12,10 +12,13 @@ across ranks (rank r renders global iterations r+1, r+1+N, ...: weak scaling) an
 float3 accumulation images are summed on rank 0 with one RCCL reduce over xGMI inside
 the timed region.
 
-Roofline: the dominant kernel is the fused bounce kernel (k_bounce); HBM-bound by
-SURVEY.md 8(d): algorithmic bytes per segment B = 352 + 52*N_aabb + 36*N_tri + 40*N_hit
-(counts from an untimed counting iteration), achieved = bytes per launch / average launch
-time measured with HIP events on the kernel's own stream during the timed steps.
+Roofline: the dominant kernel is the intersect kernel (k_trace: analytic geoms + KD traversal,
+the reference's pathTraceOneBounce*).  HBM-bound; algorithmic bytes per segment are SURVEY.md
+8(d)'s B = 352 + 52*N_aabb + 36*N_tri + 40*N_hit restricted to the intersect kernel:
+B_trace = 76 + 52*N_aabb + 36*N_tri + 40*N_hit (PathSegment read 56 + ShadeableIntersection
+write 20, plus the tree/triangle bytes), with N_* from an untimed counting iteration; achieved =
+B_trace x segments per launch / the average launch time measured with HIP events on the
+kernel's own stream during the timed steps.
 """
 from __future__ import annotations
 
@@ -135,7 +138,7 @@ def main():
     # roofline of the dominant kernel (k_bounce), per launch
     # counting iteration: aabb/tri/hit for its segments
     count_seg = max(1, sum(cnt_stats.seg_per_bounce[d] for d in range(32)) or seg // max(1, args.steps * world))
-    per_seg_bytes = 352 + 52 * aabb / count_seg + 36 * tri / count_seg + 40 * hit / count_seg
+    per_seg_bytes = 76 + 52 * aabb / count_seg + 36 * tri / count_seg + 40 * hit / count_seg
     avg_launch_ms = kernel_ms / max(1, launches)
     seg_per_launch = seg / max(1, launches)
     bytes_per_launch = per_seg_bytes * seg_per_launch
@@ -167,7 +170,7 @@ def main():
         "primary_rays_per_s": round(W * H * args.steps * world / dt, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_bounce (intersect + KD traversal + scatter + shade + gather)",
+                     "kernel": "k_trace (intersect: analytic geoms + KD traversal)",
                      "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
                      "bytes_per_segment": round(per_seg_bytes, 2),
                      "per_segment_counts": {"aabb": round(aabb / count_seg, 4), "tri": round(tri / count_seg, 4),
