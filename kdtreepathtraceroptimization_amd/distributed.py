@@ -1,0 +1,35 @@
+"""Samples-per-pixel sharding over ranks.
+
+One process per GPU.  Rank r of N renders the global iterations 1 + k*N + r (k = 0, 1, ...), so every
+iteration-dependent behaviour of the reference -- the RNG seed makeSeededRandomEngine(iter, ...), the
+iteration-2 sort, cacherays -- sees the same global iteration number it would on one GPU.  Each rank
+accumulates its own float3 sum; the only exchange is one reduce of the W*H*3 sums to rank 0 (RCCL over xGMI
+with the "nccl" backend, gloo on CPU).  No data-path collective: the shards are independent.
+"""
+from __future__ import annotations
+
+
+def global_iteration(step: int, world: int, rank: int) -> int:
+    """1-based global iteration rendered by `rank` at its local step `step`."""
+    return 1 + step * world + rank
+
+
+def shard_iterations(first_step: int, steps: int, world: int, rank: int) -> list:
+    """The global iterations of local steps [first_step, first_step + steps) on `rank`."""
+    return [global_iteration(s, world, rank) for s in range(first_step, first_step + steps)]
+
+
+def reduce_image(image, dist, dst: int = 0):
+    """Sum the ranks' accumulation buffers into `dst` (in place on `image`, a torch tensor)."""
+    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
+        dist.reduce(image, dst=dst, op=dist.ReduceOp.SUM)
+    return image
+
+
+def render_shard(tracer, first_step: int, steps: int, world: int, rank: int) -> int:
+    """Trace this rank's iterations with a PathTracer (accumulating into its image); returns segments."""
+    seg = 0
+    for it in shard_iterations(first_step, steps, world, rank):
+        tracer.trace_iteration(it)
+        seg += tracer.stats().segments
+    return seg

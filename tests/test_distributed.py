@@ -1,0 +1,69 @@
+"""Multi-rank (gloo, world_size 2, CPU) test of the spp-sharded path of bench.py / distributed.py.
+
+Each rank renders its shard of global iterations (the oracle stands in for the GPU renderer, since this
+container has no GPU), accumulates a float32 sum, and the sums are reduced to rank 0.  The result must equal
+the same shard grouping summed on one process bit for bit, and the sequential 1-rank sum within float
+summation order."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from kdtreepathtraceroptimization_amd.distributed import global_iteration, reduce_image, shard_iterations
+from kdtreepathtraceroptimization_amd.fixtures import load_fixture_scene
+
+RES = (24, 24)
+STEPS = 2  # per rank
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _render(its):
+    import oracle_lib
+    s = oracle_lib.OracleScene.from_description(load_fixture_scene("cornell", "sphere_low_1", res=RES, depth=8))
+    acc = np.zeros((RES[1], RES[0], 3), dtype=np.float32)
+    for it in its:
+        im, _ = s.render(it, 1, nthreads=1)
+        acc += im
+    return acc
+
+
+def _worker(rank, world, port, out):
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        acc = torch.from_numpy(_render(shard_iterations(0, STEPS, world, rank)).reshape(-1).copy())
+        reduce_image(acc, dist)
+        if rank == 0:
+            np.save(out, acc.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_global_iterations_partition():
+    world, steps = 4, 5
+    its = sorted(it for r in range(world) for it in shard_iterations(0, steps, world, r))
+    assert its == list(range(1, world * steps + 1))
+    assert global_iteration(0, 1, 0) == 1
+
+
+def test_sharded_reduce_world2(tmp_path, oracle):
+    world = 2
+    out = str(tmp_path / "img.npy")
+    mp.spawn(_worker, args=(world, _free_port(), out), nprocs=world, join=True)
+    got = np.load(out)
+    parts = [_render(shard_iterations(0, STEPS, world, r)).reshape(-1) for r in range(world)]
+    expect = parts[0].copy()
+    for p in parts[1:]:
+        expect += p
+    assert np.array_equal(got.view(np.uint32), expect.view(np.uint32))
+    seq = _render(range(1, world * STEPS + 1)).reshape(-1)
+    assert np.allclose(got, seq, rtol=1e-5, atol=1e-5)
