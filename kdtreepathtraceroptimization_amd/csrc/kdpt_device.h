@@ -49,7 +49,22 @@ struct DevGeom {
   float transform[16];
   float inverseTransform[16];
   float invTranspose[16];
+  // world-space bounds of the unit cube / sphere under `transform`, enlarged by a margin far above
+  // float rounding: a ray that misses them cannot hit the object (used to skip the exact test)
+  float wlo[4], whi[4];
 };
+
+// Conservative skip test for the analytic geoms (invdir finite).  The exact object-space test
+// (boxIntersectionTest / sphereIntersectionTest) reports a hit only for rays passing within rounding
+// distance of the object, ahead of the origin; the bounds carry a margin far above that.
+KDPT_HD bool geom_may_hit(const DevGeom& G, f3 o, f3 invdir) {
+  const float t1x = (G.wlo[0] - o.x) * invdir.x, t2x = (G.whi[0] - o.x) * invdir.x;
+  const float t1y = (G.wlo[1] - o.y) * invdir.y, t2y = (G.whi[1] - o.y) * invdir.y;
+  const float t1z = (G.wlo[2] - o.z) * invdir.z, t2z = (G.whi[2] - o.z) * invdir.z;
+  const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
+  const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+  return tmax >= tmin && tmax >= 0.0f;
+}
 
 struct DevScene {
   const DevGeom* geoms;
@@ -74,6 +89,18 @@ struct DevScene {
   const int* obj_material_offsets;
   // children of nodes[0] and nodes[1] for the hybrid skip line (-1 when absent)
   int n0_left, n0_right, n1_left, n1_right;
+  // big leaves (>= BIG_LEAF triangles) as clusters of <= 64 triangles in Morton order, each with its
+  // box: leaf_cl[node] = {first cluster, count} (count 0: not big); cl_lo/cl_hi boxes; cl_info =
+  // {first triangle, size}; cluster-order copies of v0/e1/e2 with the original index in e1.w
+  const int2* leaf_cl;
+  const float4* cl_lo;
+  const float4* cl_hi;
+  const int2* cl_info;
+  const float4* c_v0;
+  const float4* c_e1;
+  const float4* c_e2;
+  float4 rlo, rhi;  // the KD root's box (trace-order classes only; not used for results)
+  int trace_mode;   // 1 class+octant, 2 octant, 3 class (experiments)
   int trip_limit;  // bound on node steps per ray (a valid tree needs < 4 per node)
   int* fault;      // set to 1 when a ray exceeds trip_limit (never for a validated tree)
 };
@@ -329,6 +356,24 @@ KDPT_HD void traverseKD(const DevScene& S, const Ray& ray, Hit& h, int material_
 //   hit record    = FIRST triangle reaching the minimum t with t > 0 && t_min > t
 //   skip marks    = applied min(#intersected, 2) times (idempotent from the 2nd on)
 // ---------------------------------------------------------------------------
+// Trace-order class of a ray (a scheduling key only -- results never depend on it): rays that start
+// inside the KD root's box first (they walk the dense part of the tree), then rays that cross it, then
+// rays that miss it; within a class by direction octant so that a wave's rays step alike.
+constexpr int TRACE_KEYS = 24;
+__device__ inline int trace_class(const DevScene& S, f3 o, f3 d) {
+  const float4 lo = S.rlo, hi = S.rhi;
+  const bool inside = o.x >= lo.x && o.x <= hi.x && o.y >= lo.y && o.y <= hi.y && o.z >= lo.z && o.z <= hi.z;
+  const float ix = 1.0f / d.x, iy = 1.0f / d.y, iz = 1.0f / d.z;
+  const float t1x = (lo.x - o.x) * ix, t2x = (hi.x - o.x) * ix;
+  const float t1y = (lo.y - o.y) * iy, t2y = (hi.y - o.y) * iy;
+  const float t1z = (lo.z - o.z) * iz, t2z = (hi.z - o.z) * iz;
+  const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
+  const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+  const int cls = inside ? 0 : ((tmax >= tmin && tmax >= 0.0f) ? 1 : 2);
+  const int oct = (d.x < 0.0f ? 1 : 0) | (d.y < 0.0f ? 2 : 0) | (d.z < 0.0f ? 4 : 0);
+  return S.trace_mode == 2 ? oct : (S.trace_mode == 3 ? cls : cls * 8 + oct);
+}
+
 // ---------------------------------------------------------------------------
 // Node sources.  The traversal reads one node per step; where it reads it from
 // is a template parameter:
@@ -427,6 +472,35 @@ __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
   return v;
 }
 
+__device__ inline unsigned long long wave_max_u64(unsigned long long v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const unsigned long long o = __shfl_xor(v, off);
+    v = o > v ? o : v;
+  }
+  return v;
+}
+__device__ inline int wave_max_i32(int v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
+  return v;
+}
+
+// May the LINE through o (both directions: glm's u/v tests ignore the sign of t) cross the cluster's
+// triangles?  The box is widened by 1e-4 x (distance + size), orders of magnitude above the rounding
+// of the Moller-Trumbore u/v tests, so a culled cluster holds no triangle that would pass them.
+__device__ inline bool cluster_may_pass(float4 lo, float4 hi, f3 o, f3 inv) {
+  const float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
+  const float m = 1e-4f * (1.0f + fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) + (hi.x - lo.x) +
+                           (hi.y - lo.y) + (hi.z - lo.z));
+  const float t1x = (lo.x - m - o.x) * inv.x, t2x = (hi.x + m - o.x) * inv.x;
+  const float t1y = (lo.y - m - o.y) * inv.y, t2y = (hi.y + m - o.y) * inv.y;
+  const float t1z = (lo.z - m - o.z) * inv.z, t2z = (hi.z + m - o.z) * inv.z;
+  const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
+  const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+  return tmin <= tmax;
+}
+
 __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
@@ -499,7 +573,7 @@ __device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const Ra
   while (true) {
     // ---------------- node phase ----------------
     bool leaf = false;
-    int lstart = 0, lsize = 0;
+    int lstart = 0, lsize = 0, lparent = -1, lnode = 0;
     bool lfirst = true;
     int trips = 0;
     if (COUNT) prof_lap(W, -1);
@@ -525,7 +599,6 @@ __device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const Ra
       float dd;
       const bool hg = fastAABB ? intersectAABB_fast(o, invdir, nd.b0, nd.b1, dd)
                                : intersectAABB(o, invdir, nd.b0, nd.b1, dd);
-      if (COUNT && walk && !(isRoot && curVis && !(fl & F_HITGEOM))) cnt.aabb++;
       const bool up = curVis || !hg || dd > bz;
       const bool leftFirst = HYBRID ? (comp(d, nd.axis) > 0.0f) : true;
       const uint32_t fside = leftFirst ? 0u : 1u;
@@ -535,29 +608,36 @@ __device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const Ra
       const bool takeSecond = second != -1 && !((cl >> (fside ^ 1u)) & 1u);
       const bool descend = !up && (takeFirst || takeSecond);
       const uint32_t nside = takeFirst ? fside : (fside ^ 1u);
+      const bool lf = !up && !descend && nd.triSize > 0;
+      // "Mark and stay" on a node without triangles is always followed by a trip on the same
+      // node that finds it visited and climbs (same box, so same hitGeom): do both now.
+      const bool stay = !up && !descend && !lf;
+      const bool climb = up || stay;
+      if (COUNT && walk) cnt.aabb += (isRoot && curVis && !(fl & F_HITGEOM)) ? 0u : (stay ? 2u : 1u);
       // nodeIDs[ID] = true unless descending; nodeIDs[left] = nodeIDs[right] = true when climbing
       uint32_t ncb = cb | ((!descend && L > 0) ? (1u << vb) : 0u);
-      ncb |= up ? ((left != -1 ? 1u : 0u) | (right != -1 ? 2u : 0u)) << ((2u * Lu) & 31u) : 0u;
+      ncb |= climb ? ((left != -1 ? 1u : 0u) | (right != -1 ? 2u : 0u)) << ((2u * Lu) & 31u) : 0u;
       const uint32_t dcb = (ncb & ~(3u << ((2u * Lu + 2u) & 31u))) | ((L == 0 && nside == 0u) ? (g << 2) : 0u);
       const bool runaway = guard >= S.trip_limit;
-      const bool lf = !up && !descend && nd.triSize > 0;
       uint32_t nfl = fl & ~(F_HITGEOM | F_LFIRST);
       nfl |= (!descend && L == 0) ? F_ROOTV : 0u;
-      nfl |= (up && (left == -1 || right == -1)) ? F_SINK : 0u;
+      nfl |= (climb && (left == -1 || right == -1)) ? F_SINK : 0u;
       nfl |= hg ? F_HITGEOM : 0u;
-      nfl |= ((isRoot && up) || runaway) ? F_DONE : 0u;
+      nfl |= ((isRoot && climb) || runaway) ? F_DONE : 0u;
       nfl |= runaway ? F_FAULT : 0u;
       nfl |= lf ? F_LEAF : 0u;
       nfl |= leftFirst ? F_LFIRST : 0u;
       if (walk) {  // commit (selects)
         cb = descend ? dcb : ncb;
         ps = descend ? ((ps & ~(1u << (Lu & 31u))) | (nside << (Lu & 31u))) : ps;
-        cur = up ? nd.parent : (descend ? (takeFirst ? first : second) : cur);
-        L += descend ? 1 : (up ? -1 : 0);
+        cur = climb ? nd.parent : (descend ? (takeFirst ? first : second) : cur);
+        L += descend ? 1 : (climb ? -1 : 0);
         guard++;
         fl = nfl;
         lstart = nd.triStart;
         lsize = nd.triSize;
+        lparent = nd.parent;
+        lnode = cur;
       }
     }
     rootv = (fl & F_ROOTV) != 0u;
@@ -587,81 +667,63 @@ __device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const Ra
     // (a) big leaves: the whole wave sweeps one leaf at a time with a uniform ray
     const bool big = leaf && lsize >= BIG_LEAF;
     unsigned long long bigmask = __ballot(big);
-    if (bigmask) {
-      // Sweeps of 64 triangles over every big leaf of the wave in turn, the next sweep's
-      // triangles loaded while the current one is tested.
-      int j = __builtin_ctzll(bigmask);
+    while (bigmask) {
+      // One big leaf at a time, the whole wave on it with that lane's ray: clusters whose box the
+      // ray's line misses are skipped (when every invdir is finite), the others tested 64 at a time.
+      // Recombination by ORIGINAL index: last u/v pass = max index, last hit = max, best = min (t, index).
+      const int j = __builtin_ctzll(bigmask);
       bigmask &= bigmask - 1;
-      int jstart = __shfl(lstart, j), jsize = __shfl(lsize, j);
-      f3 jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
-      f3 jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
-      int base = 0;
-      TriData nxt = tri_load(S, jstart + min(lane, jsize - 1));
-      int u_pass = 0, u_lasthit = -1, u_nhit = 0;
-      float u_bz = 0.0f;
-      unsigned long long u_best = ~0ull;
-      while (true) {
+      const int jnode = __builtin_amdgcn_readfirstlane(__shfl(lnode, j));
+      const f3 jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
+      const f3 jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
+      const f3 jinv = mk3(__shfl(invdir.x, j), __shfl(invdir.y, j), __shfl(invdir.z, j));
+      const int2 cr = S.leaf_cl[jnode];
+      unsigned long long u_pass = 0ull, u_best = ~0ull;
+      int u_lasthit = -1, u_nhit = 0;
+      for (int cb0 = 0; cb0 < cr.y; cb0 += 64) {
+       // lane k culls cluster cb0 + k: one parallel pass over the boxes, then only the survivors
+       const int ck = cr.x + cb0 + lane;
+       const bool cv = cb0 + lane < cr.y;
+       unsigned long long cmask = __ballot(cv && (!fastAABB || cluster_may_pass(S.cl_lo[cv ? ck : cr.x],
+                                                                                 S.cl_hi[cv ? ck : cr.x], jo, jinv)));
+       while (cmask) {
+        const int c = cr.x + cb0 + __builtin_ctzll(cmask);
+        cmask &= cmask - 1;
         if (COUNT) prof_add(W, PROF_BIG_SWEEPS, 1);
-        const TriData cur_t = nxt;
-        const int cj = j, cstart = jstart, cbase = base;
-        const bool cin = base + lane < jsize;
-        const f3 co = jo, cd = jd;
-        // advance to the next sweep (this leaf or the next big leaf) and start its loads
-        base += 64;
-        bool more = true, leaf_end = false;
-        if (base >= jsize) {
-          leaf_end = true;
-          if (bigmask) {
-            j = __builtin_ctzll(bigmask);
-            bigmask &= bigmask - 1;
-            jstart = __shfl(lstart, j);
-            jsize = __shfl(lsize, j);
-            jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
-            jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
-            base = 0;
-          } else {
-            more = false;
-          }
-        }
-        if (more) nxt = tri_load(S, jstart + min(base + lane, jsize - 1));
-        // test the current sweep
-        const int tri = cstart + cbase + lane;
+        const int2 ci = S.cl_info[c];
+        const bool in = lane < ci.y;
+        const int ct = ci.x + (in ? lane : 0);
+        const TriData T{S.c_v0[ct], S.c_e1[ct], S.c_e2[ct]};
+        const int orig = fbits(T.e1.w);
         float bx = 0, by = 0, bzk = 0;
-        const int r = cin ? tri_test_v(cur_t, co, cd, bx, by, bzk) : 0;
-        const unsigned long long m1 = __ballot(r >= 1);
-        if (m1) {
-          const int last = 63 - __builtin_clzll(m1);
-          u_pass = cstart + cbase + last + 1;
-          u_bz = __shfl(bzk, last);
+        const int r = in ? tri_test_v(T, jo, jd, bx, by, bzk) : 0;
+        if (__ballot(r >= 1)) {
+          const unsigned long long pk =
+              r >= 1 ? ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk) : 0ull;
+          const unsigned long long wm = wave_max_u64(pk);
+          u_pass = wm > u_pass ? wm : u_pass;
           const unsigned long long m2 = __ballot(r == 2);
           if (m2) {
-            u_lasthit = cstart + cbase + 63 - __builtin_clzll(m2);
             u_nhit += __builtin_popcountll(m2);
+            u_lasthit = max(u_lasthit, wave_max_i32(r == 2 ? orig : -1));
             unsigned long long key = ~0ull;
             if (r == 2) {
               f3 hp, nn;
-              const float t = tri_hit_t<HYBRID>(S, tri, co, cd, bx, by, bzk, hp, nn);
-              if (t > 0.0f) key = ((unsigned long long)f2u(t) << 32) | (unsigned int)tri;
+              const float t = tri_hit_t<HYBRID>(S, orig, jo, jd, bx, by, bzk, hp, nn);
+              if (t > 0.0f) key = ((unsigned long long)f2u(t) << 32) | (unsigned int)orig;
             }
-            const unsigned long long wm = wave_min_u64(key);
-            u_best = wm < u_best ? wm : u_best;
+            const unsigned long long wb = wave_min_u64(key);
+            u_best = wb < u_best ? wb : u_best;
           }
         }
-        if (leaf_end) {
-          if (lane == cj) {
-            r_pass = u_pass;
-            r_bz = u_bz;
-            r_lasthit = u_lasthit;
-            r_nhit = u_nhit;
-            r_best = u_best;
-          }
-          u_pass = 0;
-          u_lasthit = -1;
-          u_nhit = 0;
-          u_bz = 0.0f;
-          u_best = ~0ull;
-        }
-        if (!more) break;
+       }
+      }
+      if (lane == j) {
+        r_pass = (int)(u_pass >> 32);
+        r_bz = u2f((uint32_t)(u_pass & 0xffffffffu));
+        r_lasthit = u_lasthit;
+        r_nhit = u_nhit;
+        r_best = u_best;
       }
     }
     if (COUNT) prof_lap(W, PROF_BIG_CYC);
@@ -774,6 +836,13 @@ __device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const Ra
           }
         }
       }
+      // The reference's next trip finds the leaf visited and climbs (leaves have no children,
+      // validated: nodeIDs[-1] = true twice); do it here instead of in the node phase.
+      if (COUNT) cnt.aabb++;
+      sink = true;
+      done = cur == S.root;
+      cur = lparent;
+      L--;
     }
     if (COUNT) prof_lap(W, PROF_FINAL_CYC);
   }

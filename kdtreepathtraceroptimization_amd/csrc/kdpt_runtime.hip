@@ -139,6 +139,7 @@ constexpr int TRACE_BLOCK = 1024;
 struct TraceArgs {
   DevScene S;
   PathBuf paths;
+  const int* perm;  // trace order (chunk slot -> path index), or null for identity
   int2* hits;
   const int* counts;
   int* work;  // [cap] chunk counters, zeroed by k_gen_rays
@@ -195,8 +196,9 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
     if (chunk * 64 >= n) break;  // uniform
     const unsigned long long t_k0 = COUNT ? __builtin_readcyclecounter() : 0ull;
     if (COUNT) prof_lap(W, -1);
-    const int i = chunk * 64 + lane;
-    const bool valid = i < n;
+    const int slot = chunk * 64 + lane;
+    const bool valid = slot < n;
+    const int i = (A.perm && valid) ? A.perm[slot] : slot;
     float4 q0 = make_float4(0, 0, 0, 0), q1 = make_float4(0, 0, 1, 0);
     int bounces = 0;
     if (valid) {
@@ -221,10 +223,17 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
     if (active) {
       f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
       float t = 0;
+      const f3 inv = mk3(1.0f / ray.direction.x, 1.0f / ray.direction.y, 1.0f / ray.direction.z);
+      const bool finite = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
       for (int g = 0; g < S.num_geoms; g++) {
         const DevGeom& G = S.geoms[g];
-        if (G.type == 1) t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
-        else if (G.type == 0) t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+        if (finite && !geom_may_hit(G, ray.origin, inv)) {
+          t = -1.0f;  // the exact test would miss
+        } else if (G.type == 1) {
+          t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
+        } else if (G.type == 0) {
+          t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+        }
         if (t > 0.0f && h.t_min > t) {
           h.t_min = t;
           h.hit_geom_index = g;
@@ -272,6 +281,7 @@ struct ShadeArgs {
   float softness;
   int enable_sss;
   int* tile_counts;  // [ntiles] or key-major [MAX_KEYS][ntiles] when sorting
+  int* tile_kcounts;  // key-major [TRACE_KEYS][ntiles] survivors per trace-order class, or null
   int ntiles;
   int nkeys;
   unsigned long long* total_segments;  // running sum of paths launched into the intersect kernel
@@ -285,10 +295,12 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   const int i = tile * TILE + threadIdx.x;
   if (i == 0) atomicAdd(A.total_segments, (unsigned long long)n);
   __shared__ int s_hist[MAX_KEYS];
+  __shared__ int s_khist[TRACE_KEYS];
   if (SORT) {
     for (int k = threadIdx.x; k < MAX_KEYS; k += TILE) s_hist[k] = 0;
-    __syncthreads();
   }
+  if (COMPACT && A.tile_kcounts && threadIdx.x < TRACE_KEYS) s_khist[threadIdx.x] = 0;
+  if (SORT || (COMPACT && A.tile_kcounts)) __syncthreads();
   const DevScene& S = A.S;
   bool alive = false;
   int key = 0;
@@ -345,6 +357,11 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
     }
     alive = COMPACT ? (bounces != 0) : true;
     key = matHit;
+    if (COMPACT && A.tile_kcounts && alive) atomicAdd(&s_khist[trace_class(S, ray.origin, ray.direction)], 1);
+  }
+  if (COMPACT && A.tile_kcounts) {
+    __syncthreads();
+    if (threadIdx.x < TRACE_KEYS) A.tile_kcounts[threadIdx.x * A.ntiles + tile] = s_khist[threadIdx.x];
   }
   if (SORT) {
     if (alive) atomicAdd(&s_hist[key], 1);
@@ -358,7 +375,7 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
 
 // Exclusive scan of the tile counts (one workgroup; <= MAX_KEYS * ntiles entries).
 __global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ tile_counts, int* __restrict__ tile_off,
-                                               int* counts, int depth, int ntiles_alloc, int nkeys) {
+                                               int* counts, int depth, int ntiles_alloc, int nkeys, int write_total) {
   const int n = counts[depth];
   const int ntiles = (n + TILE - 1) / TILE;
   const int total_entries = nkeys * ntiles;
@@ -400,13 +417,15 @@ __global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ tile_coun
     if (threadIdx.x == 1023) s_carry = excl + v;
     __syncthreads();
   }
-  if (threadIdx.x == 0) counts[depth + 1] = s_carry;
+  if (threadIdx.x == 0 && write_total) counts[depth + 1] = s_carry;
 }
 
 // Stable compaction (and, on iter 2, the stable sort by materialIdHit).
 template <bool SORT>
 __global__ __launch_bounds__(TILE) void k_scatter(PathBuf src, PathBuf dst, const int* __restrict__ tile_off,
-                                                  const int* counts, int depth, int ntiles_alloc, int compact) {
+                                                  const int* counts, int depth, int ntiles_alloc, int compact,
+                                                  const int* __restrict__ ktile_off, int* __restrict__ perm,
+                                                  DevScene S) {
   const int n = counts[depth];
   const int tile = blockIdx.x;
   if (tile * TILE >= n) return;
@@ -445,6 +464,28 @@ __global__ __launch_bounds__(TILE) void k_scatter(PathBuf src, PathBuf dst, cons
     dst.p1[dst_i] = q1;
     dst.p2[dst_i] = q2;
     dst.pm[dst_i] = pm;
+  }
+  if (perm) {
+    // next bounce's trace order: stable by trace_class (the keys k_shade counted), tile-major
+    __shared__ int s_kc[TILE / 64][TRACE_KEYS];
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    for (int k = lane; k < TRACE_KEYS; k += 64) s_kc[wid][k] = 0;
+    const int key = alive ? trace_class(S, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z)) : 0;
+    int rank = 0;
+    unsigned long long rem = __ballot(alive);
+    while (rem) {  // one round per distinct key in the wave
+      const int k = __shfl(key, __builtin_ctzll(rem));
+      const unsigned long long m = __ballot(alive && key == k);
+      if (alive && key == k) rank = (int)lane_prefix(m);
+      if (lane == 0) s_kc[wid][k] = __popcll(m);
+      rem &= ~m;
+    }
+    __syncthreads();
+    if (alive) {
+      int before = 0;
+      for (int w = 0; w < wid; w++) before += s_kc[w][key];
+      perm[ktile_off[key * ntiles_alloc + tile] + before + rank] = dst_i;
+    }
   }
 }
 
@@ -541,6 +582,10 @@ struct kdpt_ctx {
   size_t tree_lds = 0;    // dynamic LDS bytes of the intersect kernel (TREE_LDS)
   int* tile_counts = nullptr;
   int* tile_off = nullptr;
+  int* tile_kcounts = nullptr;  // trace-order class counts per tile [TRACE_KEYS][ntiles]
+  int* tile_koff = nullptr;
+  int* perm = nullptr;          // trace order of the next bounce
+  bool trace_order = true;      // KDPT_TRACE_ORDER=0 disables (identity order)
   Counters* counters = nullptr;
   Counters last_profile{};
   unsigned long long* total_segments = nullptr;  // device running total (async use)
@@ -572,6 +617,81 @@ int dupload(kdpt_ctx* c, T** p, const T* src, size_t n) {
 }
 
 int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count);
+
+// Big leaves as clusters of <= 64 triangles (kdpt_device.h DevScene::leaf_cl ...): Morton order of
+// the triangle centroids inside the leaf's box, consecutive runs of 64, each with its exact float box.
+// Only the order in which the wave tests a big leaf's triangles changes; results are recombined by
+// original index, so any grouping is exact.
+int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>& tv, const std::vector<float4>& e1,
+                   const std::vector<float4>& e2) {
+  const int nn = sc->num_nodes;
+  std::vector<int2> leaf_cl(nn, make_int2(0, 0));
+  std::vector<float4> lo, hi, cv0, ce1, ce2;
+  std::vector<int2> info;
+  auto spread = [](uint32_t v) {
+    uint32_t r = 0;
+    for (int b = 0; b < 10; b++) r |= ((v >> b) & 1u) << (3 * b);
+    return r;
+  };
+  for (int i = 0; i < nn; i++) {
+    const kdpt_node_bare& N = sc->nodes[i];
+    if (N.triIdSize < BIG_LEAF) continue;
+    const int start = N.triIdStart, size = N.triIdSize;
+    std::vector<std::pair<uint32_t, int>> key(size);
+    for (int k = 0; k < size; k++) {
+      const kdpt_tri_bare& T = sc->tris[start + k];
+      const double cen[3] = {(T.x1 + (double)T.x2 + T.x3) / 3, (T.y1 + (double)T.y2 + T.y3) / 3,
+                             (T.z1 + (double)T.z2 + T.z3) / 3};
+      uint32_t m = 0;
+      for (int a = 0; a < 3; a++) {
+        const double ext = std::max((double)N.maxs[a] - N.mins[a], 1e-30);
+        const double u = std::min(std::max((cen[a] - N.mins[a]) / ext, 0.0), 1.0);
+        m |= spread((uint32_t)(u * 1023.0)) << a;
+      }
+      key[k] = {m, k};
+    }
+    std::stable_sort(key.begin(), key.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
+    leaf_cl[i] = make_int2((int)info.size(), (size + 63) / 64);
+    for (int b = 0; b < size; b += 64) {
+      const int cnt = std::min(64, size - b);
+      float l[3] = {FLT_MAXV, FLT_MAXV, FLT_MAXV}, h[3] = {-FLT_MAXV, -FLT_MAXV, -FLT_MAXV};
+      info.push_back(make_int2((int)cv0.size(), cnt));
+      for (int k = b; k < b + cnt; k++) {
+        const int t = start + key[k].second;
+        const kdpt_tri_bare& T = sc->tris[t];
+        const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
+        for (int v = 0; v < 3; v++) {
+          l[0] = std::min(l[0], vx[v]); h[0] = std::max(h[0], vx[v]);
+          l[1] = std::min(l[1], vy[v]); h[1] = std::max(h[1], vy[v]);
+          l[2] = std::min(l[2], vz[v]); h[2] = std::max(h[2], vz[v]);
+        }
+        cv0.push_back(tv[t]);
+        float4 q = e1[t];
+        q.w = ibits(t);  // original triangle index
+        ce1.push_back(q);
+        ce2.push_back(e2[t]);
+      }
+      lo.push_back(make_float4(l[0], l[1], l[2], 0.0f));
+      hi.push_back(make_float4(h[0], h[1], h[2], 0.0f));
+    }
+  }
+  int2 *dl, *di;
+  float4 *dlo, *dhi, *dv0, *de1, *de2;
+  int rc;
+  if ((rc = dupload(c, &dl, leaf_cl.data(), leaf_cl.size())) || (rc = dupload(c, &di, info.data(), info.size())) ||
+      (rc = dupload(c, &dlo, lo.data(), lo.size())) || (rc = dupload(c, &dhi, hi.data(), hi.size())) ||
+      (rc = dupload(c, &dv0, cv0.data(), cv0.size())) || (rc = dupload(c, &de1, ce1.data(), ce1.size())) ||
+      (rc = dupload(c, &de2, ce2.data(), ce2.size())))
+    return rc;
+  c->S.leaf_cl = dl;
+  c->S.cl_info = di;
+  c->S.cl_lo = dlo;
+  c->S.cl_hi = dhi;
+  c->S.c_v0 = dv0;
+  c->S.c_e1 = de1;
+  c->S.c_e2 = de2;
+  return KDPT_OK;
+}
 
 // NodesPacked records (kdpt_device.h); false when the tree does not fit the format.
 bool pack_nodes(const kdpt_node_bare* N, int nn, std::vector<int4>& out) {
@@ -710,6 +830,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
           return fail(KDPT_ERR_ARG, "inconsistent KD node links");
       if (N[i].triIdSize > 0 && (N[i].triIdStart < 0 || N[i].triIdStart + N[i].triIdSize > sc->num_tris))
         return fail(KDPT_ERR_ARG, "triangle range out of bounds");
+      if (N[i].triIdSize > 0 && (N[i].leftID != -1 || N[i].rightID != -1))
+        return fail(KDPT_ERR_UNSUPPORTED, "KD node with both triangles and children");
     }
     if (sc->num_nodes > 1 && N[0].leftID != 1) return fail(KDPT_ERR_UNSUPPORTED, "node 1 must be root's left child");
     level.assign(sc->num_nodes, 0);
@@ -751,6 +873,25 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     memcpy(dg[i].transform, sc->geoms[i].transform, 64);
     memcpy(dg[i].inverseTransform, sc->geoms[i].inverseTransform, 64);
     memcpy(dg[i].invTranspose, sc->geoms[i].invTranspose, 64);
+    {  // world bounds of the transformed unit cube (contains the transformed unit sphere), + margin
+      const float* m = sc->geoms[i].transform;  // column-major
+      double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+      for (int k = 0; k < 8; k++) {
+        const double v[3] = {(k & 1) ? 0.5 : -0.5, (k & 2) ? 0.5 : -0.5, (k & 4) ? 0.5 : -0.5};
+        for (int r = 0; r < 3; r++) {
+          const double w = (double)m[r] * v[0] + (double)m[4 + r] * v[1] + (double)m[8 + r] * v[2] + (double)m[12 + r];
+          lo[r] = std::min(lo[r], w);
+          hi[r] = std::max(hi[r], w);
+        }
+      }
+      const double ext = std::max(std::max(hi[0] - lo[0], hi[1] - lo[1]), hi[2] - lo[2]);
+      const double margin = 1e-3 * ext + 1e-3;
+      for (int r = 0; r < 3; r++) {
+        dg[i].wlo[r] = (float)(lo[r] - margin);
+        dg[i].whi[r] = (float)(hi[r] + margin);
+      }
+      dg[i].wlo[3] = dg[i].whi[3] = 0.0f;
+    }
     if (dg[i].materialid < 0 || dg[i].materialid >= sc->num_materials)
       return bail(fail(KDPT_ERR_ARG, "geom materialid out of range"));
   }
@@ -821,6 +962,7 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
       if ((rc = dupload(c, &dp, packed.data(), packed.size()))) return bail(rc);
       c->S.pnodes = dp;
     }
+    if ((rc = build_clusters(c, sc, tv, e1, e2))) return bail(rc);
     c->S.tv0 = dtv;
     c->S.te1 = de1;
     c->S.te2 = de2;
@@ -828,6 +970,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     c->S.tn1 = dn1;
     c->S.tn2 = dn2;
     c->S.obj_material_offsets = doff;
+    c->S.rlo = make_float4(sc->nodes[0].mins[0], sc->nodes[0].mins[1], sc->nodes[0].mins[2], 0.0f);
+    c->S.rhi = make_float4(sc->nodes[0].maxs[0], sc->nodes[0].maxs[1], sc->nodes[0].maxs[2], 0.0f);
     c->S.n0_left = sc->nodes[0].leftID;
     c->S.n0_right = sc->nodes[0].rightID;
     if (nn > 1) {
@@ -850,7 +994,9 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     return bail(rc);
   }
   // counts[0..cap+1]: live paths per bounce (rewritten every iteration); counts[cap+2]: fault flag
-  if ((rc = dalloc(c, &c->counts, 2 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) || (rc = dalloc(c, &c->tile_counts, (size_t)MAX_KEYS * c->ntiles)) ||
+  if ((rc = dalloc(c, &c->counts, 2 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
+      (rc = dalloc(c, &c->perm, (size_t)c->npix)) || (rc = dalloc(c, &c->tile_kcounts, (size_t)TRACE_KEYS * c->ntiles)) ||
+      (rc = dalloc(c, &c->tile_koff, (size_t)TRACE_KEYS * c->ntiles)) || (rc = dalloc(c, &c->tile_counts, (size_t)MAX_KEYS * c->ntiles)) ||
       (rc = dalloc(c, &c->tile_off, (size_t)MAX_KEYS * c->ntiles)) || (rc = dalloc(c, &c->counters, 1)) ||
       (rc = dalloc(c, &c->total_segments, 1)))
     return bail(rc);
@@ -862,6 +1008,9 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   {
     const char* e = getenv("KDPT_SYNC_DEBUG");
     c->sync_debug = e && e[0] == '1';
+    const char* t = getenv("KDPT_TRACE_ORDER");
+    c->S.trace_mode = t ? atoi(t) : 0;
+    c->trace_order = c->S.trace_mode > 0 && c->S.has_obj && c->S.num_nodes > 0;
   }
   if ((rc = setup_trace(c))) return bail(rc);
   c->S.trip_limit = 8 * std::max(c->S.num_nodes, 1) + 64;
@@ -1150,6 +1299,7 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
     TraceArgs t;
     t.S = c->S;
     t.paths = c->buf[c->cur];
+    t.perm = (depth > 0 && compact && c->trace_order) ? c->perm : nullptr;
     t.hits = c->hits;
     t.counts = c->counts;
     t.work = c->work;
@@ -1176,6 +1326,7 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
     a.softness = c->opt.softness;
     a.enable_sss = c->opt.enable_sss;
     a.tile_counts = c->tile_counts;
+    a.tile_kcounts = (compact && c->trace_order) ? c->tile_kcounts : nullptr;
     a.ntiles = c->ntiles;
     a.nkeys = c->nkeys;
     a.total_segments = c->total_segments;
@@ -1188,15 +1339,22 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
     }
     if (compact || sort) {
       hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, c->stream, c->tile_counts, c->tile_off, c->counts, depth,
-                         c->ntiles, sort ? c->nkeys : 1);
+                         c->ntiles, sort ? c->nkeys : 1, 1);
       HIP_TRY(hipGetLastError());
+      const bool order = compact && c->trace_order;
+      if (order) {
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, c->stream, c->tile_kcounts, c->tile_koff, c->counts,
+                           depth, c->ntiles, TRACE_KEYS, 0);
+        HIP_TRY(hipGetLastError());
+      }
       const int nxt = c->cur ^ 1;
+      int* perm = order ? c->perm : nullptr;
       if (sort)
         hipLaunchKernelGGL(k_scatter<true>, dim3(c->ntiles), dim3(TILE), 0, c->stream, c->buf[c->cur], c->buf[nxt],
-                           c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0);
+                           c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, c->tile_koff, perm, c->S);
       else
         hipLaunchKernelGGL(k_scatter<false>, dim3(c->ntiles), dim3(TILE), 0, c->stream, c->buf[c->cur], c->buf[nxt],
-                           c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0);
+                           c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, c->tile_koff, perm, c->S);
       HIP_TRY(hipGetLastError());
       c->cur = nxt;
     } else {
