@@ -30,6 +30,10 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
+# kdpt_trace_iterations keeps `--pipeline` iterations in flight on their own HIP streams plus one
+# accumulation stream; HIP's default of 4 hardware queues per process would make some of them share
+# a queue (and serialise), so ask for 8 before the runtime initialises.
+os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -47,6 +51,8 @@ def parse():
     ap.add_argument("--bare", action="store_true", help="traverseKDbare instead of the short-stack hybrid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--pipeline", type=int, default=3,
+                    help="iterations in flight (kdpt_trace_iterations; bit-identical to one at a time)")
     return ap.parse_args()
 
 
@@ -98,32 +104,31 @@ def main():
         return global_iteration(step, world, rank)
 
     # warmup (iterations disjoint from the timed ones); iteration 2's extra sort lands here
-    for w in range(args.warmup):
-        pt.trace_iteration(global_iter(w))
+    if args.warmup:
+        pt.trace_iterations(global_iter(0), args.warmup, stride=world, pipeline=args.pipeline)
+        pt.synchronize()
     # roofline counters from one untimed counting iteration of the timed range
     aabb, tri, hit = pt.count_iteration(global_iter(args.warmup))
     cnt_stats = pt.stats()
     accum.zero_()
     torch.cuda.synchronize()
+    st0 = pt.stats()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    seg = 0
-    kernel_ms = 0.0
-    launches = 0
-    for k in range(args.steps):
-        pt.trace_iteration(global_iter(args.warmup + k))
-        st = pt.stats()
-        seg += st.segments
-        kernel_ms += st.ms_intersect
-        launches += st.bounces
+    pt.trace_iterations(global_iter(args.warmup), args.steps, stride=world, pipeline=args.pipeline)
+    pt.synchronize()
     reduce_image(accum, dist)  # spp shards -> one framebuffer (the only exchange step)
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     dt = time.perf_counter() - t0
+    st1 = pt.stats()
+    seg = st1.total_segments - st0.total_segments
+    kernel_ms = st1.intersect_ms_total - st0.intersect_ms_total
+    launches = st1.intersect_launches_total - st0.intersect_launches_total
     if dist:
         t = torch.tensor([dt, float(seg), kernel_ms, float(launches)], dtype=torch.float64, device=f"cuda:{local}")
         tmax = t[0:1].clone()
@@ -163,7 +168,8 @@ def main():
         "data": "synthetic camera rays over the reference's own scene assets (cornell.txt + dragon_5.obj, "
                 "parsed fixtures under tests/golden); deterministic RNG seeded by iteration",
         "config": {"workload": f"{args.scene}.txt + {args.mesh}.obj, {W}x{H}, depth {args.depth}, 1 spp per step "
-                               f"per GPU, short-stack hybrid KD traversal" if not args.bare else "bare traversal",
+                               f"per GPU ({args.pipeline} iterations in flight), "
+                               + ("short-stack hybrid KD traversal" if not args.bare else "bare traversal"),
                    "scene": args.scene, "mesh": args.mesh, "resolution": [W, H], "depth": args.depth,
                    "kd_nodes": sd.view.num_nodes, "kd_tri_refs": sd.view.num_tris,
                    "parallelism": f"spp-sharded x{world} + RCCL reduce" if world > 1 else "single GPU"},
@@ -173,6 +179,7 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "k_trace (intersect: analytic geoms + KD traversal)",
                      "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
+                     "aggregate_GBps": round(per_seg_bytes * seg / dt / 1e9, 2),
                      "bytes_per_segment": round(per_seg_bytes, 2),
                      "per_segment_counts": {"aabb": round(aabb / count_seg, 4), "tri": round(tri / count_seg, 4),
                                             "hit": round(hit / count_seg, 5)}},

@@ -156,6 +156,8 @@ typedef struct kdpt_stats {
     float ms_last_iteration;     /* hipEvent time of the last kdpt_trace_iteration (gen .. last gather) */
     float ms_intersect;          /* testing_mode: sum of intersect-kernel time, last iteration */
     long long total_segments;    /* since create/reset */
+    double intersect_ms_total;   /* testing_mode: intersect-kernel time summed over launches since reset */
+    long long intersect_launches_total; /* ... and the number of those launches */
 } kdpt_stats;
 
 typedef struct kdpt_ctx kdpt_ctx;
@@ -167,6 +169,11 @@ int kdpt_create(const kdpt_scene *scene, const kdpt_options *opt, int device, kd
 /* pathtrace(pbo, frame, iter, ...): one iteration (1 sample per pixel); iter is 1-based and
  * seeds the RNG.  Synchronous on return, like the reference. */
 int kdpt_trace_iteration(kdpt_ctx *ctx, int frame, int iter);
+/* Iterations first_iter + k*stride (k < count), `pipeline` of them in flight at once (each on its own
+ * stream and buffers; partial images added into the image in iteration order, so the result is
+ * bit-identical to calling kdpt_trace_iteration for each).  Returns after enqueueing; follow with
+ * kdpt_synchronize.  Stats: iterations, total_segments and the intersect totals. */
+int kdpt_trace_iterations(kdpt_ctx *ctx, int frame, int first_iter, int count, int stride, int pipeline);
 /* As kdpt_trace_iteration but returns after enqueueing (no host sync, no stats). */
 int kdpt_trace_iteration_async(kdpt_ctx *ctx, int frame, int iter);
 int kdpt_synchronize(kdpt_ctx *ctx);
@@ -185,13 +192,15 @@ int kdpt_image_device_ptr(kdpt_ctx *ctx, void **dptr);
  * live PathSegment array (reference layout) to host `out` (>= W*H entries). */
 int kdpt_debug_paths(kdpt_ctx *ctx, int iter, int stop_depth, kdpt_path_segment *out, int *npaths);
 /* Roofline counters: one extra, untimed iteration that also counts AABB tests, triangle
- * tests and triangle hits (aabb_tri_hit[3]); the image is not touched. */
+ * tests and triangle hits (aabb_tri_hit[3]); the image is not touched.  Afterwards kdpt_get_stats
+ * reports that iteration's segments and seg_per_bounce. */
 int kdpt_count_iteration(kdpt_ctx *ctx, int iter, unsigned long long *aabb_tri_hit);
 /* Diagnostic: cycle profile of the intersect kernel during the last kdpt_count_iteration.
  * Copies up to n values -- node trips, node cycles, big-leaf sweeps, big-leaf cycles,
  * small-leaf phases, small-leaf rounds, small-leaf cycles, recombination cycles, setup
  * cycles, analytic-geometry cycles, post cycles, spare (each summed over 64-path chunks),
- * chunks, chunk cycles, aabb, tri, hit -- and returns how many exist. */
+ * chunks, chunk cycles, aabb, tri, hit, then a 64-bin histogram of intersect-wave lifetimes
+ * (10 us bins) -- and returns how many exist. */
 int kdpt_wave_profile(kdpt_ctx *ctx, unsigned long long *out, int n);
 /* Device-math known answers: sinf/cosf/pow-5 Fresnel/u01 evaluated by the gfx950 code. */
 int kdpt_selftest_math(const float *x, int n, float *sin_out, float *cos_out);

@@ -93,6 +93,7 @@ struct DevScene {
   // box: leaf_cl[node] = {first cluster, count} (count 0: not big); cl_lo/cl_hi boxes; cl_info =
   // {first triangle, size}; cluster-order copies of v0/e1/e2 with the original index in e1.w
   const int2* leaf_cl;
+  int num_clusters;
   const float4* cl_lo;
   const float4* cl_hi;
   const int2* cl_info;
@@ -101,6 +102,7 @@ struct DevScene {
   const float4* c_e2;
   float4 rlo, rhi;  // the KD root's box (trace-order classes only; not used for results)
   int trace_mode;   // 1 class+octant, 2 octant, 3 class (experiments)
+  int early_walk, early_leaf;  // leaf phase starts when <= early_walk lanes walk and >= early_leaf wait
   int trip_limit;  // bound on node steps per ray (a valid tree needs < 4 per node)
   int* fault;      // set to 1 when a ray exceeds trip_limit (never for a validated tree)
 };
@@ -393,6 +395,7 @@ struct NodeRec {
 };
 
 struct NodesWide {
+  static constexpr bool kLeafHoldsCluster = false;  // big leaves: clusters from DevScene::leaf_cl
   const int4* p;
   __device__ NodeRec operator()(int i) const {
     const int4 q0 = p[4 * i], q1 = p[4 * i + 1], q2 = p[4 * i + 2];
@@ -412,6 +415,7 @@ struct NodesWide {
 __device__ inline int link16(uint32_t v) { return v == 0xffffu ? -1 : (int)v; }
 
 struct NodesPacked {
+  static constexpr bool kLeafHoldsCluster = true;  // big leaves: triStart holds the first cluster
   const int4* p;  // global or LDS (address space inferred after inlining)
   __device__ NodeRec operator()(int i) const {
     const int4 q0 = p[2 * i], q1 = p[2 * i + 1];
@@ -434,6 +438,19 @@ struct NodesPacked {
 enum ProfSlot {
   PROF_NODE_TRIPS, PROF_NODE_CYC, PROF_BIG_SWEEPS, PROF_BIG_CYC, PROF_SMALL_PHASES, PROF_SMALL_ROUNDS,
   PROF_SMALL_CYC, PROF_FINAL_CYC, PROF_SETUP_CYC, PROF_GEOM_CYC, PROF_POST_CYC, PROF_SPARE, PROF_SLOTS
+};
+
+// Cluster boxes of the big leaves: separate lo/hi arrays (HBM) or interleaved lo, hi (LDS copy).
+struct ClustersSplit {
+  const float4* lo;
+  const float4* hi;
+  __device__ float4 lo_of(int c) const { return lo[c]; }
+  __device__ float4 hi_of(int c) const { return hi[c]; }
+};
+struct ClustersInterleaved {
+  const float4* p;
+  __device__ float4 lo_of(int c) const { return p[2 * c]; }
+  __device__ float4 hi_of(int c) const { return p[2 * c + 1]; }
 };
 
 struct WaveLeafLDS {
@@ -550,9 +567,9 @@ __device__ inline float tri_hit_t(const DevScene& S, int i, f3 o, f3 d, float bx
   return distance(o, hit);
 }
 
-template <bool HYBRID, bool COUNT, typename NodeSrc>
-__device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const Ray& ray, bool active, Hit& h,
-                               int material_size, TraverseCounters& cnt, WaveLeafLDS* W) {
+template <bool HYBRID, bool COUNT, typename NodeSrc, typename ClusterSrc>
+__device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const ClusterSrc& clusters, const Ray& ray,
+                               bool active, Hit& h, int material_size, TraverseCounters& cnt, WaveLeafLDS* W) {
   int objTri = -1;  // returned: the triangle whose hit record won (valid when h.obj_intersect)
   const int lane = threadIdx.x & 63;
   const f3 o = ray.origin, d = ray.direction;
@@ -588,7 +605,11 @@ __device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const Ra
                   F_LFIRST;
     while (true) {
       const bool walk = (fl & (F_DONE | F_LEAF)) == 0u;
-      if (!__any(walk)) break;
+      const unsigned long long wmask = __ballot(walk);
+      if (!wmask) break;
+      // Few lanes still walking and many waiting on leaves: test those leaves now; the walkers keep
+      // their state and resume in the next node phase (their own sequence of steps is unchanged).
+      if (__popcll(wmask) <= S.early_walk && __popcll(__ballot((fl & F_LEAF) != 0u)) >= S.early_leaf) break;
       if (COUNT) trips += walk ? 1 : 0;
       const NodeRec nd = nodes(cur < 0 ? 0 : cur);
       const int left = nd.left, right = nd.right;
@@ -673,19 +694,22 @@ __device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const Ra
       // Recombination by ORIGINAL index: last u/v pass = max index, last hit = max, best = min (t, index).
       const int j = __builtin_ctzll(bigmask);
       bigmask &= bigmask - 1;
-      const int jnode = __builtin_amdgcn_readfirstlane(__shfl(lnode, j));
+      const int jfirst = __builtin_amdgcn_readfirstlane(
+          NodeSrc::kLeafHoldsCluster ? __shfl(lstart, j) : S.leaf_cl[__shfl(lnode, j)].x);
+      const int jcount = (__builtin_amdgcn_readfirstlane(__shfl(lsize, j)) + 63) >> 6;
       const f3 jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
       const f3 jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
       const f3 jinv = mk3(__shfl(invdir.x, j), __shfl(invdir.y, j), __shfl(invdir.z, j));
-      const int2 cr = S.leaf_cl[jnode];
+      const int2 cr = make_int2(jfirst, jcount);
       unsigned long long u_pass = 0ull, u_best = ~0ull;
       int u_lasthit = -1, u_nhit = 0;
       for (int cb0 = 0; cb0 < cr.y; cb0 += 64) {
        // lane k culls cluster cb0 + k: one parallel pass over the boxes, then only the survivors
        const int ck = cr.x + cb0 + lane;
        const bool cv = cb0 + lane < cr.y;
-       unsigned long long cmask = __ballot(cv && (!fastAABB || cluster_may_pass(S.cl_lo[cv ? ck : cr.x],
-                                                                                 S.cl_hi[cv ? ck : cr.x], jo, jinv)));
+       const int cq = cv ? ck : cr.x;
+       unsigned long long cmask =
+           __ballot(cv && (!fastAABB || cluster_may_pass(clusters.lo_of(cq), clusters.hi_of(cq), jo, jinv)));
        while (cmask) {
         const int c = cr.x + cb0 + __builtin_ctzll(cmask);
         cmask &= cmask - 1;

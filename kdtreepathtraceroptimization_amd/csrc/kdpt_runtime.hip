@@ -61,6 +61,7 @@ struct PathBuf {
 struct Counters {
   unsigned long long aabb, tri, hit;
   unsigned long long wave[PROF_SLOTS + 2];  // WaveLeafLDS::prof summed over chunks, then chunks, cycles
+  unsigned long long life[64];  // count mode: wave lifetimes in the intersect kernel, 10 us bins (s_memrealtime)
 };
 
 __device__ inline unsigned int lane_prefix(unsigned long long mask) {
@@ -140,6 +141,11 @@ struct TraceArgs {
   DevScene S;
   PathBuf paths;
   const int* perm;  // trace order (chunk slot -> path index), or null for identity
+  // with perm: class starts in the trace order = koff[(k * keys_per_class) * ntiles_alloc], and the
+  // chunk width of each class (heavy classes get narrow chunks: their leaf work adds up per wave)
+  const int* koff;
+  int ntiles_alloc, keys_per_class, nclass;
+  int cw[3];
   int2* hits;
   const int* counts;
   int* work;  // [cap] chunk counters, zeroed by k_gen_rays
@@ -178,12 +184,18 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
     if (n == 0) return;  // uniform: nothing to trace
     const int words = 2 * S.num_nodes;
     for (int k = threadIdx.x; k < words; k += TRACE_BLOCK) s_tree[k] = S.pnodes[k];
+    float4* s_cl = reinterpret_cast<float4*>(s_tree + words);
+    for (int k = threadIdx.x; k < S.num_clusters; k += TRACE_BLOCK) {
+      s_cl[2 * k] = S.cl_lo[k];
+      s_cl[2 * k + 1] = S.cl_hi[k];
+    }
     __syncthreads();
   }
   const int lane = threadIdx.x & 63;
   WaveLeafLDS* W = &s_leaf[threadIdx.x >> 6];
   if (COUNT && lane < PROF_SLOTS) W->prof[lane] = 0;
   int* work = A.work + A.depth;
+  const unsigned long long rt0 = COUNT ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // First chunk: the wave's own index (no atomic -- thousands of waves start at once);
   // later chunks from the shared counter, which starts past the statically taken ones.
   const int nwaves = gridDim.x * (TRACE_BLOCK / 64);
@@ -193,11 +205,35 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
       atomicOr(S.fault, 4);
       break;
     }
-    if (chunk * 64 >= n) break;  // uniform
+    // chunk -> [base, end) of trace-order slots
+    int base = chunk * A.cw[2], end = min(n, base + A.cw[2]);
+    if (A.koff) {
+      int c = chunk, cls = 0;
+      base = n;
+      end = n;
+      for (; cls < A.nclass; cls++) {
+        const int s0 = A.koff[cls * A.keys_per_class * A.ntiles_alloc];
+        const int s1 = cls + 1 < A.nclass ? A.koff[(cls + 1) * A.keys_per_class * A.ntiles_alloc] : n;
+        const int nc = (s1 - s0 + A.cw[cls] - 1) / A.cw[cls];
+        if (c < nc) {
+          base = s0 + c * A.cw[cls];
+          end = min(s1, base + A.cw[cls]);
+          break;
+        }
+        c -= nc;
+      }
+    }
+    if (base >= n) {  // uniform
+      if (COUNT && lane == 0) {
+        const unsigned long long us10 = (__builtin_amdgcn_s_memrealtime() - rt0) / 1000;  // 100 MHz ticks
+        atomicAdd(&A.counters->life[us10 < 63 ? us10 : 63], 1ull);
+      }
+      break;
+    }
     const unsigned long long t_k0 = COUNT ? __builtin_readcyclecounter() : 0ull;
     if (COUNT) prof_lap(W, -1);
-    const int slot = chunk * 64 + lane;
-    const bool valid = slot < n;
+    const int slot = base + lane;
+    const bool valid = slot < end;
     const int i = (A.perm && valid) ? A.perm[slot] : slot;
     float4 q0 = make_float4(0, 0, 0, 0), q1 = make_float4(0, 0, 1, 0);
     int bounces = 0;
@@ -245,11 +281,14 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
     int objTri = -1;
     if (S.has_obj && S.num_nodes > 0) {  // uniform: every lane of the wave takes part
       if (MODE == TREE_LDS)
-        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesPacked{s_tree}, ray, active, h, S.num_materials, cnt, W);
+        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesPacked{s_tree}, ClustersInterleaved{reinterpret_cast<const float4*>(s_tree + 2 * S.num_nodes)},
+                                                ray, active, h, S.num_materials, cnt, W);
       else if (MODE == TREE_PACKED)
-        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ray, active, h, S.num_materials, cnt, W);
+        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ClustersSplit{S.cl_lo, S.cl_hi}, ray, active, h,
+                                                S.num_materials, cnt, W);
       else
-        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesWide{S.nodes}, ray, active, h, S.num_materials, cnt, W);
+        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesWide{S.nodes}, ClustersSplit{S.cl_lo, S.cl_hi}, ray, active, h,
+                                                S.num_materials, cnt, W);
     }
     if (valid && active) {
       const int code = h.hit_geom_index == -1 ? -1 : (h.obj_intersect ? -(objTri + 2) : h.hit_geom_index);
@@ -586,6 +625,7 @@ struct kdpt_ctx {
   int* tile_koff = nullptr;
   int* perm = nullptr;          // trace order of the next bounce
   bool trace_order = true;      // KDPT_TRACE_ORDER=0 disables (identity order)
+  int chunk_width[3] = {16, 64, 64};
   Counters* counters = nullptr;
   Counters last_profile{};
   unsigned long long* total_segments = nullptr;  // device running total (async use)
@@ -595,6 +635,19 @@ struct kdpt_ctx {
   kdpt_stats stats{};
   bool count_mode = false;
   bool sync_debug = false;  // KDPT_SYNC_DEBUG=1: synchronise and log after every launch
+  // Pipelined iterations (kdpt_trace_iterations): extra slots, each a context sharing this one's
+  // scene upload but owning its per-iteration buffers, stream and partial image; the partial
+  // images are added into `image` in iteration order on `accum_stream`.
+  kdpt_ctx* parent = nullptr;
+  std::vector<kdpt_ctx*> slots;
+  std::vector<hipEvent_t> slot_done, slot_free;
+  hipStream_t accum_stream = nullptr;
+  // intersect-kernel timing (testing_mode) of every iteration, read back at synchronisation
+  std::vector<std::vector<hipEvent_t>> pending_ev;  // per launched iteration: 2 events per bounce
+  std::vector<hipEvent_t> free_ev;
+  std::vector<hipEvent_t>* rec_ev = nullptr;  // when set, launch_iteration records the bounce events here
+  double intersect_ms_total = 0;
+  long long intersect_launches_total = 0;
 };
 
 namespace {
@@ -618,14 +671,128 @@ int dupload(kdpt_ctx* c, T** p, const T* src, size_t n) {
 
 int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count);
 
+// stats.segments / seg_per_bounce / bounces of the iteration whose counts are in h_counts
+int segments_from_counts(kdpt_ctx* c) {
+  long long seg = 0;
+  int bounces = 0;
+  for (int d = 0; d < 32; d++) c->stats.seg_per_bounce[d] = 0;
+  for (int d = 0; d < c->cap; d++) {
+    const int nd = c->h_counts[d];
+    if (d > 0 && c->h_counts[d] <= 0) break;  // the reference stops once num_paths <= 0
+    seg += nd;
+    if (d < 32) c->stats.seg_per_bounce[d] = nd;
+    bounces = d + 1;
+    if (c->opt.compaction && c->h_counts[d + 1] <= 0) break;
+  }
+  c->stats.segments = seg;
+  c->stats.bounces = bounces;
+  return bounces;
+}
+
+// Per-iteration device state: two path buffers, hit records, trace order, tile counts/offsets,
+// live counts + fault word + work counters.  (The scene, image and counters live elsewhere.)
+int alloc_iteration_buffers(kdpt_ctx* c) {
+  int rc;
+  for (int b = 0; b < 2; b++) {
+    if ((rc = dalloc(c, &c->buf[b].p0, c->npix)) || (rc = dalloc(c, &c->buf[b].p1, c->npix)) ||
+        (rc = dalloc(c, &c->buf[b].p2, c->npix)) || (rc = dalloc(c, &c->buf[b].pm, c->npix)))
+      return rc;
+    HIP_TRY(hipMemset(c->buf[b].pm, 0, sizeof(int) * c->npix));
+  }
+  // counts[0..cap+1]: live paths per bounce (rewritten every iteration); counts[cap+2]: fault flag;
+  // counts[cap+3 ..]: work counters of the persistent intersect kernel
+  if ((rc = dalloc(c, &c->counts, 2 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
+      (rc = dalloc(c, &c->perm, (size_t)c->npix)) ||
+      (rc = dalloc(c, &c->tile_kcounts, (size_t)TRACE_KEYS * c->ntiles)) ||
+      (rc = dalloc(c, &c->tile_koff, (size_t)TRACE_KEYS * c->ntiles)) ||
+      (rc = dalloc(c, &c->tile_counts, (size_t)MAX_KEYS * c->ntiles)) ||
+      (rc = dalloc(c, &c->tile_off, (size_t)MAX_KEYS * c->ntiles)))
+    return rc;
+  if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 3), hipHostMallocDefault) != hipSuccess)
+    return fail(KDPT_ERR_HIP, "hipHostMalloc");
+  HIP_TRY(hipMemset(c->counts, 0, sizeof(int) * (2 * c->cap + 3)));
+  c->S.fault = c->counts + c->cap + 2;
+  c->work = c->counts + c->cap + 3;
+  return KDPT_OK;
+}
+
+int alloc_iteration_events(kdpt_ctx* c) {
+  HIP_TRY(hipEventCreate(&c->ev0));
+  HIP_TRY(hipEventCreate(&c->ev1));
+  c->bounce_ev.resize(2 * (size_t)c->cap);
+  for (auto& e : c->bounce_ev) HIP_TRY(hipEventCreate(&e));
+  return KDPT_OK;
+}
+
+// A pipeline slot: shares p's scene upload and counters, owns its iteration buffers, its stream
+// and a partial image that k_gen_rays' iteration accumulates into.
+int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
+  kdpt_ctx* c = new kdpt_ctx();
+  c->parent = p;
+  c->device = p->device;
+  c->opt = p->opt;
+  c->opt.external_image = nullptr;
+  c->cam = p->cam;
+  c->traceDepth = p->traceDepth;
+  c->W = p->W;
+  c->H = p->H;
+  c->npix = p->npix;
+  c->ntiles = p->ntiles;
+  c->nkeys = p->nkeys;
+  c->cap = p->cap;
+  c->S = p->S;
+  c->tree_mode = p->tree_mode;
+  c->trace_grid = p->trace_grid;
+  c->tree_lds = p->tree_lds;
+  c->trace_order = p->trace_order;
+  for (int k = 0; k < 3; k++) c->chunk_width[k] = p->chunk_width[k];
+  c->counters = p->counters;
+  c->total_segments = p->total_segments;
+  c->sync_debug = p->sync_debug;
+  int rc;
+  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+    kdpt_destroy(c);
+    return fail(KDPT_ERR_HIP, "hipStreamCreate failed");
+  }
+  if ((rc = alloc_iteration_buffers(c)) || (rc = dalloc(c, &c->image, 3 * (size_t)c->npix)) ||
+      (rc = alloc_iteration_events(c))) {
+    kdpt_destroy(c);
+    return rc;
+  }
+  *out = c;
+  return KDPT_OK;
+}
+
+__global__ void k_accumulate(float* __restrict__ image, const float* __restrict__ part, int n3) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i < n3) image[i] += part[i];  // one add per pixel and iteration, as partialGather does
+}
+
+// Read back the intersect-kernel events of finished iterations (testing_mode).
+int drain_intersect_events(kdpt_ctx* c) {
+  for (auto& evs : c->pending_ev) {
+    for (size_t k = 0; k + 1 < evs.size(); k += 2) {
+      float ms = 0;
+      HIP_TRY(hipEventSynchronize(evs[k + 1]));
+      if (hipEventElapsedTime(&ms, evs[k], evs[k + 1]) == hipSuccess) {
+        c->intersect_ms_total += ms;
+        c->intersect_launches_total++;
+      }
+    }
+    for (auto e : evs) c->free_ev.push_back(e);
+  }
+  c->pending_ev.clear();
+  return KDPT_OK;
+}
+
 // Big leaves as clusters of <= 64 triangles (kdpt_device.h DevScene::leaf_cl ...): Morton order of
 // the triangle centroids inside the leaf's box, consecutive runs of 64, each with its exact float box.
 // Only the order in which the wave tests a big leaf's triangles changes; results are recombined by
 // original index, so any grouping is exact.
 int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>& tv, const std::vector<float4>& e1,
-                   const std::vector<float4>& e2) {
+                   const std::vector<float4>& e2, std::vector<int2>& leaf_cl) {
   const int nn = sc->num_nodes;
-  std::vector<int2> leaf_cl(nn, make_int2(0, 0));
+  leaf_cl.assign(nn, make_int2(0, 0));
   std::vector<float4> lo, hi, cv0, ce1, ce2;
   std::vector<int2> info;
   auto spread = [](uint32_t v) {
@@ -684,6 +851,7 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
       (rc = dupload(c, &de2, ce2.data(), ce2.size())))
     return rc;
   c->S.leaf_cl = dl;
+  c->S.num_clusters = (int)info.size();
   c->S.cl_info = di;
   c->S.cl_lo = dlo;
   c->S.cl_hi = dhi;
@@ -694,7 +862,7 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
 }
 
 // NodesPacked records (kdpt_device.h); false when the tree does not fit the format.
-bool pack_nodes(const kdpt_node_bare* N, int nn, std::vector<int4>& out) {
+bool pack_nodes(const kdpt_node_bare* N, int nn, const std::vector<int2>& leaf_cl, std::vector<int4>& out) {
   if (nn >= 0xffff) return false;
   out.assign(2 * (size_t)nn, make_int4(0, 0, 0, 0));
   auto l16 = [](int v) { return v == -1 ? 0xffffu : (uint32_t)v; };
@@ -703,7 +871,9 @@ bool pack_nodes(const kdpt_node_bare* N, int nn, std::vector<int4>& out) {
     const bool tris = n.triIdSize > 0;
     if (tris && (n.leftID != -1 || n.rightID != -1 || n.triIdSize >= (1 << 13))) return false;
     const uint32_t axis = n.axis == 0 ? 0u : (n.axis == 1 ? 1u : 2u);  // comp(): anything else reads z
-    const uint32_t w6 = tris ? (uint32_t)n.triIdStart : (l16(n.leftID) | (l16(n.rightID) << 16));
+    // a big leaf keeps its first cluster instead of its first triangle (its clusters carry the triangles)
+    const uint32_t first = n.triIdSize >= BIG_LEAF ? (uint32_t)leaf_cl[i].x : (uint32_t)n.triIdStart;
+    const uint32_t w6 = tris ? first : (l16(n.leftID) | (l16(n.rightID) << 16));
     const uint32_t w7 = l16(n.parentID) | (axis << 16) | ((tris ? 1u : 0u) << 18) |
                         ((tris ? (uint32_t)n.triIdSize : 0u) << 19);
     out[2 * i] = make_int4(fbits(n.mins[0]), fbits(n.mins[1]), fbits(n.mins[2]), fbits(n.maxs[0]));
@@ -728,7 +898,7 @@ int setup_trace(kdpt_ctx* c) {
   c->tree_mode = c->S.pnodes ? TREE_PACKED : TREE_WIDE;
   c->tree_lds = 0;
   const size_t static_lds = sizeof(WaveLeafLDS) * (TRACE_BLOCK / 64);
-  const size_t tree_bytes = 32 * (size_t)c->S.num_nodes;
+  const size_t tree_bytes = 32 * (size_t)c->S.num_nodes + 32 * (size_t)c->S.num_clusters;  // + cluster boxes
   const size_t lds_max = prop.sharedMemPerBlock > 0 ? prop.sharedMemPerBlock : 65536;
   if (c->S.pnodes && static_lds + tree_bytes <= lds_max) {
     c->tree_mode = TREE_LDS;
@@ -956,13 +1126,14 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
       return bail(rc);
     c->S.nodes = dnodes;
     c->S.pnodes = nullptr;
+    std::vector<int2> leaf_cl;
+    if ((rc = build_clusters(c, sc, tv, e1, e2, leaf_cl))) return bail(rc);
     std::vector<int4> packed;
-    if (pack_nodes(sc->nodes, nn, packed)) {
+    if (pack_nodes(sc->nodes, nn, leaf_cl, packed)) {
       int4* dp;
       if ((rc = dupload(c, &dp, packed.data(), packed.size()))) return bail(rc);
       c->S.pnodes = dp;
     }
-    if ((rc = build_clusters(c, sc, tv, e1, e2))) return bail(rc);
     c->S.tv0 = dtv;
     c->S.te1 = de1;
     c->S.te2 = de2;
@@ -981,44 +1152,31 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   } else {
     c->S.has_obj = 0;
   }
-  for (int b = 0; b < 2; b++) {
-    if ((rc = dalloc(c, &c->buf[b].p0, c->npix)) || (rc = dalloc(c, &c->buf[b].p1, c->npix)) ||
-        (rc = dalloc(c, &c->buf[b].p2, c->npix)) || (rc = dalloc(c, &c->buf[b].pm, c->npix)))
-      return bail(rc);
-    if (hipMemset(c->buf[b].pm, 0, sizeof(int) * c->npix) != hipSuccess) return bail(fail(KDPT_ERR_HIP, "memset"));
-  }
+  if ((rc = alloc_iteration_buffers(c))) return bail(rc);
   if (o.external_image) {
     c->image = o.external_image;
     c->image_external = true;
   } else if ((rc = dalloc(c, &c->image, 3 * (size_t)c->npix))) {
     return bail(rc);
   }
-  // counts[0..cap+1]: live paths per bounce (rewritten every iteration); counts[cap+2]: fault flag
-  if ((rc = dalloc(c, &c->counts, 2 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
-      (rc = dalloc(c, &c->perm, (size_t)c->npix)) || (rc = dalloc(c, &c->tile_kcounts, (size_t)TRACE_KEYS * c->ntiles)) ||
-      (rc = dalloc(c, &c->tile_koff, (size_t)TRACE_KEYS * c->ntiles)) || (rc = dalloc(c, &c->tile_counts, (size_t)MAX_KEYS * c->ntiles)) ||
-      (rc = dalloc(c, &c->tile_off, (size_t)MAX_KEYS * c->ntiles)) || (rc = dalloc(c, &c->counters, 1)) ||
-      (rc = dalloc(c, &c->total_segments, 1)))
-    return bail(rc);
-  if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 3), hipHostMallocDefault) != hipSuccess)
-    return bail(fail(KDPT_ERR_HIP, "hipHostMalloc"));
-  if (hipMemset(c->counts, 0, sizeof(int) * (2 * c->cap + 3)) != hipSuccess) return bail(fail(KDPT_ERR_HIP, "memset"));
-  c->S.fault = c->counts + c->cap + 2;
-  c->work = c->counts + c->cap + 3;
+  if ((rc = dalloc(c, &c->counters, 1)) || (rc = dalloc(c, &c->total_segments, 1))) return bail(rc);
   {
     const char* e = getenv("KDPT_SYNC_DEBUG");
     c->sync_debug = e && e[0] == '1';
     const char* t = getenv("KDPT_TRACE_ORDER");
     c->S.trace_mode = t ? atoi(t) : 0;
+    c->S.early_walk = 0;
+    c->S.early_leaf = 65;
+    const char* ew = getenv("KDPT_EARLY_LEAF");  // "walkers,leaves", e.g. "8,16"
+    if (ew) sscanf(ew, "%d,%d", &c->S.early_walk, &c->S.early_leaf);
+    const char* cw = getenv("KDPT_CHUNK_WIDTHS");  // e.g. "16,32,64"
+    if (cw) sscanf(cw, "%d,%d,%d", &c->chunk_width[0], &c->chunk_width[1], &c->chunk_width[2]);
+    for (int k = 0; k < 3; k++) c->chunk_width[k] = std::min(64, std::max(1, c->chunk_width[k]));
     c->trace_order = c->S.trace_mode > 0 && c->S.has_obj && c->S.num_nodes > 0;
   }
   if ((rc = setup_trace(c))) return bail(rc);
   c->S.trip_limit = 8 * std::max(c->S.num_nodes, 1) + 64;
-  if (hipEventCreate(&c->ev0) != hipSuccess || hipEventCreate(&c->ev1) != hipSuccess)
-    return bail(fail(KDPT_ERR_HIP, "hipEventCreate"));
-  c->bounce_ev.resize(2 * (size_t)c->cap);
-  for (auto& e : c->bounce_ev)
-    if (hipEventCreate(&e) != hipSuccess) return bail(fail(KDPT_ERR_HIP, "hipEventCreate"));
+  if ((rc = alloc_iteration_events(c))) return bail(rc);
   if ((rc = kdpt_reset(c))) return bail(rc);
   *out = c;
   return KDPT_OK;
@@ -1027,6 +1185,11 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
 int kdpt_reset(kdpt_ctx* c) {
   if (!c) return fail(KDPT_ERR_ARG, "null ctx");
   HIP_TRY(hipSetDevice(c->device));
+  for (auto sl : c->slots) HIP_TRY(hipStreamSynchronize(sl->stream));
+  if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
+  drain_intersect_events(c);
+  c->intersect_ms_total = 0;
+  c->intersect_launches_total = 0;
   HIP_TRY(hipMemsetAsync(c->image, 0, sizeof(float) * 3 * (size_t)c->npix, c->stream));
   HIP_TRY(hipMemsetAsync(c->total_segments, 0, sizeof(unsigned long long), c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
@@ -1042,7 +1205,16 @@ int kdpt_trace_iteration_async(kdpt_ctx* c, int frame, int iter) {
 
 int kdpt_synchronize(kdpt_ctx* c) {
   if (!c) return fail(KDPT_ERR_ARG, "null ctx");
+  HIP_TRY(hipSetDevice(c->device));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  for (auto sl : c->slots) {
+    HIP_TRY(hipStreamSynchronize(sl->stream));
+    int rc = check_fault(sl);
+    if (rc) return rc;
+  }
+  if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
+  int rc = drain_intersect_events(c);
+  if (rc) return rc;
   return check_fault(c);
 }
 
@@ -1061,19 +1233,7 @@ int kdpt_trace_iteration(kdpt_ctx* c, int frame, int iter) {
   HIP_TRY(hipEventElapsedTime(&ms, c->ev0, c->ev1));
   c->stats.ms_last_iteration = ms;
   c->stats.iterations++;
-  long long seg = 0;
-  int bounces = 0;
-  for (int d = 0; d < 32; d++) c->stats.seg_per_bounce[d] = 0;
-  for (int d = 0; d < c->cap; d++) {
-    const int nd = c->h_counts[d];
-    if (d > 0 && c->h_counts[d] <= 0) break;  // the reference stops once num_paths <= 0
-    seg += nd;
-    if (d < 32) c->stats.seg_per_bounce[d] = nd;
-    bounces = d + 1;
-    if (c->opt.compaction && c->h_counts[d + 1] <= 0) break;
-  }
-  c->stats.segments = seg;
-  c->stats.bounces = bounces;
+  const int bounces = segments_from_counts(c);
   if (c->opt.testing_mode) {
     float tot = 0;
     for (int d = 0; d < bounces; d++) {
@@ -1081,13 +1241,71 @@ int kdpt_trace_iteration(kdpt_ctx* c, int frame, int iter) {
       if (hipEventElapsedTime(&b, c->bounce_ev[2 * d], c->bounce_ev[2 * d + 1]) == hipSuccess) tot += b;
     }
     c->stats.ms_intersect = tot;
+    c->intersect_ms_total += tot;
+    c->intersect_launches_total += bounces;
   }
+  return KDPT_OK;
+}
+
+int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int stride, int pipeline) {
+  (void)frame;
+  if (!c || count < 0 || first_iter < 1 || stride < 1) return fail(KDPT_ERR_ARG, "bad arguments");
+  if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
+  HIP_TRY(hipSetDevice(c->device));
+  const int depth = std::min(8, std::max(1, pipeline));
+  if (!c->accum_stream) HIP_TRY(hipStreamCreateWithFlags(&c->accum_stream, hipStreamNonBlocking));
+  // the accumulation follows everything already queued on the context's own stream (reset, ...)
+  hipEvent_t entry;
+  HIP_TRY(hipEventCreate(&entry));
+  HIP_TRY(hipEventRecord(entry, c->stream));
+  HIP_TRY(hipStreamWaitEvent(c->accum_stream, entry, 0));
+  while ((int)c->slots.size() < depth) {
+    kdpt_ctx* sl = nullptr;
+    int rc = make_slot(c, &sl);
+    if (rc) return rc;
+    c->slots.push_back(sl);
+    hipEvent_t d, f;
+    HIP_TRY(hipEventCreateWithFlags(&d, hipEventDisableTiming));
+    HIP_TRY(hipEventCreateWithFlags(&f, hipEventDisableTiming));
+    HIP_TRY(hipEventRecord(f, c->accum_stream));
+    c->slot_done.push_back(d);
+    c->slot_free.push_back(f);
+  }
+  for (int k = 0; k < count; k++) {
+    const int si = k % depth;
+    kdpt_ctx* sl = c->slots[si];
+    HIP_TRY(hipStreamWaitEvent(sl->stream, c->slot_free[si], 0));  // its last partial image was consumed
+    HIP_TRY(hipMemsetAsync(sl->image, 0, sizeof(float) * 3 * (size_t)c->npix, sl->stream));
+    std::vector<hipEvent_t> evs;
+    if (c->opt.testing_mode) {
+      for (int e = 0; e < 2 * c->cap; e++) {
+        hipEvent_t ev;
+        if (!c->free_ev.empty()) { ev = c->free_ev.back(); c->free_ev.pop_back(); }
+        else HIP_TRY(hipEventCreate(&ev));
+        evs.push_back(ev);
+      }
+      c->pending_ev.push_back(evs);
+      sl->rec_ev = &c->pending_ev.back();
+    }
+    int rc = launch_iteration(sl, first_iter + k * stride, -1, false);
+    sl->rec_ev = nullptr;
+    if (rc) return rc;
+    HIP_TRY(hipEventRecord(c->slot_done[si], sl->stream));
+    HIP_TRY(hipStreamWaitEvent(c->accum_stream, c->slot_done[si], 0));
+    const int n3 = 3 * c->npix;
+    hipLaunchKernelGGL(k_accumulate, dim3((n3 + 255) / 256), dim3(256), 0, c->accum_stream, c->image, sl->image, n3);
+    HIP_TRY(hipGetLastError());
+    HIP_TRY(hipEventRecord(c->slot_free[si], c->accum_stream));
+  }
+  HIP_TRY(hipEventDestroy(entry));
+  c->stats.iterations += count;
   return KDPT_OK;
 }
 
 int kdpt_read_image(kdpt_ctx* c, float* rgb) {
   if (!c || !rgb) return fail(KDPT_ERR_ARG, "null arg");
   HIP_TRY(hipSetDevice(c->device));
+  if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
   HIP_TRY(hipMemcpyAsync(rgb, c->image, sizeof(float) * 3 * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return KDPT_OK;
@@ -1113,6 +1331,8 @@ int kdpt_get_stats(kdpt_ctx* c, kdpt_stats* st) {
   HIP_TRY(hipMemcpyAsync(&tot, c->total_segments, sizeof tot, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->stats.total_segments = (long long)tot;
+  c->stats.intersect_ms_total = c->intersect_ms_total;
+  c->stats.intersect_launches_total = c->intersect_launches_total;
   *st = c->stats;
   return KDPT_OK;
 }
@@ -1127,6 +1347,14 @@ int kdpt_destroy(kdpt_ctx* c) {
   if (!c) return KDPT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
+  if (c->accum_stream) (void)hipStreamSynchronize(c->accum_stream);
+  for (auto s : c->slots) kdpt_destroy(s);
+  for (auto e : c->slot_done) (void)hipEventDestroy(e);
+  for (auto e : c->slot_free) (void)hipEventDestroy(e);
+  for (auto& evs : c->pending_ev)
+    for (auto e : evs) (void)hipEventDestroy(e);
+  for (auto e : c->free_ev) (void)hipEventDestroy(e);
+  if (c->accum_stream) (void)hipStreamDestroy(c->accum_stream);
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->h_counts) (void)hipHostFree(c->h_counts);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -1190,7 +1418,9 @@ int kdpt_count_iteration(kdpt_ctx* c, int iter, unsigned long long* aabb_tri_hit
   Counters h{};
   if (!rc) {
     HIP_TRY(hipMemcpyAsync(&h, c->counters, sizeof h, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(c->h_counts, c->counts, sizeof(int) * (c->cap + 3), hipMemcpyDeviceToHost, c->stream));
     HIP_TRY(hipStreamSynchronize(c->stream));
+    segments_from_counts(c);  // stats.segments / seg_per_bounce now describe the counting iteration
     rc = check_fault(c);
   }
   (void)hipFree(scratch);
@@ -1209,8 +1439,10 @@ int kdpt_wave_profile(kdpt_ctx* c, unsigned long long* out, int n) {
   v[PROF_SLOTS + 2] = c->last_profile.aabb;
   v[PROF_SLOTS + 3] = c->last_profile.tri;
   v[PROF_SLOTS + 4] = c->last_profile.hit;
-  for (int k = 0; k < n && k < PROF_SLOTS + 5; k++) out[k] = v[k];
-  return PROF_SLOTS + 5;
+  int k = 0;
+  for (; k < n && k < PROF_SLOTS + 5; k++) out[k] = v[k];
+  for (int b = 0; b < 64 && k < n; b++, k++) out[k] = c->last_profile.life[b];
+  return PROF_SLOTS + 5 + 64;
 }
 
 int kdpt_selftest_math(const float* x, int n, float* so, float* co) {
@@ -1300,12 +1532,18 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
     t.S = c->S;
     t.paths = c->buf[c->cur];
     t.perm = (depth > 0 && compact && c->trace_order) ? c->perm : nullptr;
+    t.koff = t.perm ? c->tile_koff : nullptr;
+    t.ntiles_alloc = c->ntiles;
+    t.keys_per_class = c->S.trace_mode == 1 ? 8 : 1;
+    t.nclass = c->S.trace_mode == 2 ? 1 : 3;
+    for (int k = 0; k < 3; k++) t.cw[k] = c->chunk_width[k];
     t.hits = c->hits;
     t.counts = c->counts;
     t.work = c->work;
     t.depth = depth;
     t.counters = c->counters;
-    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(c->bounce_ev[2 * depth], c->stream));
+    std::vector<hipEvent_t>& bev = c->rec_ev ? *c->rec_ev : c->bounce_ev;
+    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(bev[2 * depth], c->stream));
     launch_trace(c, t, count);
     HIP_TRY(hipGetLastError());
     if (c->sync_debug) {
@@ -1314,7 +1552,7 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
       HIP_TRY(hipStreamSynchronize(c->stream));
       fprintf(stderr, "[kdpt] trace depth %d done\n", depth);
     }
-    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(c->bounce_ev[2 * depth + 1], c->stream));
+    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(bev[2 * depth + 1], c->stream));
     ShadeArgs a;
     a.S = c->S;
     a.paths = c->buf[c->cur];

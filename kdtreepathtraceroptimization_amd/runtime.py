@@ -83,7 +83,8 @@ class Options(C.Structure):
 class Stats(C.Structure):
     _fields_ = [("segments", C.c_longlong), ("seg_per_bounce", C.c_longlong * 32), ("bounces", C.c_int),
                 ("iterations", C.c_int), ("ms_last_iteration", C.c_float), ("ms_intersect", C.c_float),
-                ("total_segments", C.c_longlong)]
+                ("total_segments", C.c_longlong), ("intersect_ms_total", C.c_double),
+                ("intersect_launches_total", C.c_longlong)]
 
 
 class SceneDesc(C.Structure):
@@ -100,7 +101,7 @@ assert C.sizeof(Geom) == 236 and C.sizeof(Material) == 56 and C.sizeof(Camera) =
 assert C.sizeof(NodeBare) == 64 and C.sizeof(TriBare) == 76 and C.sizeof(PathSegment) == 56
 
 EXPORTS = [
-    "kdpt_default_options", "kdpt_create", "kdpt_trace_iteration", "kdpt_trace_iteration_async", "kdpt_synchronize",
+    "kdpt_default_options", "kdpt_create", "kdpt_trace_iteration", "kdpt_trace_iteration_async", "kdpt_trace_iterations", "kdpt_synchronize",
     "kdpt_read_image", "kdpt_write_pbo", "kdpt_reset", "kdpt_get_stats", "kdpt_destroy", "kdpt_last_error",
     "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_wave_profile", "kdpt_selftest_math", "kdpt_selftest_rng",
     "kdpt_selftest_fresnel", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
@@ -128,6 +129,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_create.argtypes = [P(Scene), P(Options), C.c_int, P(C.c_void_p)]
     lib.kdpt_trace_iteration.argtypes = [C.c_void_p, C.c_int, C.c_int]
     lib.kdpt_trace_iteration_async.argtypes = [C.c_void_p, C.c_int, C.c_int]
+    lib.kdpt_trace_iterations.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
     lib.kdpt_synchronize.argtypes = [C.c_void_p]
     lib.kdpt_read_image.argtypes = [C.c_void_p, P(C.c_float)]
     lib.kdpt_write_pbo.argtypes = [C.c_void_p, C.c_int, P(C.c_uint8)]
@@ -317,6 +319,11 @@ class PathTracer:
     def trace_iteration_async(self, iteration: int, frame: int = 0):
         _check(self.lib.kdpt_trace_iteration_async(self._ctx, int(frame), int(iteration)), "kdpt_trace_iteration_async")
 
+    def trace_iterations(self, first: int, count: int, stride: int = 1, pipeline: int = 3, frame: int = 0):
+        """Iterations first + k*stride (k < count), `pipeline` in flight (kdpt_trace_iterations; async)."""
+        _check(self.lib.kdpt_trace_iterations(self._ctx, int(frame), int(first), int(count), int(stride),
+                                              int(pipeline)), "kdpt_trace_iterations")
+
     def synchronize(self):
         _check(self.lib.kdpt_synchronize(self._ctx), "kdpt_synchronize")
 
@@ -359,13 +366,16 @@ class PathTracer:
 
     def wave_profile(self):
         """Cycle profile of the intersect kernel in the last count_iteration (kdpt_wave_profile)."""
-        out = (C.c_ulonglong * 64)()
-        n = self.lib.kdpt_wave_profile(self._ctx, out, 64)
+        out = (C.c_ulonglong * 128)()
+        n = self.lib.kdpt_wave_profile(self._ctx, out, 128)
         _check(0 if n > 0 else n, "kdpt_wave_profile")
         keys = ("node_trips", "node_cycles", "big_sweeps", "big_cycles", "small_phases", "small_rounds",
                 "small_cycles", "final_cycles", "setup_cycles", "geom_cycles", "post_cycles", "spare",
                 "chunks", "chunk_cycles", "aabb", "tri", "hit")
-        return dict(zip(keys, (int(out[k]) for k in range(n))))
+        prof = dict(zip(keys, (int(out[k]) for k in range(len(keys)))))
+        if n > len(keys):
+            prof["wave_life_10us"] = [int(out[k]) for k in range(len(keys), min(n, 128))]
+        return prof
 
     def close(self):
         if self._ctx:

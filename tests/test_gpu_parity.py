@@ -184,3 +184,25 @@ def test_soft_branch_within_tolerance(kdpt, oracle, opts):
     o, _ = oracle.OracleScene.from_description(desc).render(1, 1, softness=opts["softness"])
     same = np.mean(g == o)
     assert same > 0.99, same
+
+
+@pytest.mark.parametrize("pipeline", [1, 3])
+def test_pipelined_iterations_bit_exact(kdpt, pipeline):
+    """kdpt_trace_iterations (several iterations in flight, partial images added in order) gives the
+    same image bits and segment counts as one kdpt_trace_iteration after another."""
+    desc = load_fixture_scene("cornell", "dragon_5", res=(96, 80), depth=8)
+    sd = kdpt.SceneData.from_description(desc)
+    seq = kdpt.PathTracer(sd, kdpt.default_options())
+    for it in range(1, 8):
+        seq.trace_iteration(it)
+    img_seq = seq.image()
+    tot_seq = seq.stats().total_segments
+    seq.close()
+    pip = kdpt.PathTracer(sd, kdpt.default_options())
+    pip.trace_iterations(1, 7, pipeline=pipeline)
+    pip.synchronize()
+    img_pip = pip.image()
+    tot_pip = pip.stats().total_segments
+    pip.close()
+    assert tot_pip == tot_seq
+    assert np.array_equal(img_pip.view(np.uint32), img_seq.view(np.uint32))

@@ -8,7 +8,8 @@ import torch  # noqa: F401  (loads the HIP runtime first)
 from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options, load_fixture_scene
 
 mesh = sys.argv[1] if len(sys.argv) > 1 else "dragon_5"
-for res in [(16, 16), (800, 800)]:
+RES = [(int(r), int(r)) for r in sys.argv[2].split(",")] if len(sys.argv) > 2 else [(16, 16), (800, 800)]
+for res in RES:
     sd = SceneData.from_description(load_fixture_scene("cornell", mesh, res=res, depth=8))
     pt = PathTracer(sd, default_options(testing_mode=1))
     for it in (1, 2, 3):
@@ -17,9 +18,11 @@ for res in [(16, 16), (800, 800)]:
     pt.count_iteration(3)
     p = pt.wave_profile()
     w = max(1, p["chunks"])
+    life = p.pop("wave_life_10us", [])
     per_chunk = {k: round(v / w, 1) for k, v in p.items() if k != "chunks"}
     kc = max(1, p["chunk_cycles"])
     frac = {k: round(p[k] / kc, 3) for k in p if k.endswith("_cycles") and k != "chunk_cycles"}
     print(json.dumps({"res": res, "ms_intersect": round(st.ms_intersect, 3), "chunks": p["chunks"],
-                      "per_chunk": per_chunk, "frac_of_chunk_cycles": frac}), flush=True)
+                      "per_chunk": per_chunk, "frac_of_chunk_cycles": frac,
+                      "wave_life_10us": life}), flush=True)
     pt.close()
