@@ -17,8 +17,10 @@ the reference's pathTraceOneBounce*).  HBM-bound; algorithmic bytes per segment 
 8(d)'s B = 352 + 52*N_aabb + 36*N_tri + 40*N_hit restricted to the intersect kernel:
 B_trace = 76 + 52*N_aabb + 36*N_tri + 40*N_hit (PathSegment read 56 + ShadeableIntersection
 write 20, plus the tree/triangle bytes), with N_* from an untimed counting iteration; achieved =
-B_trace x segments per launch / the average launch time measured with HIP events on the
-kernel's own stream during the timed steps.
+B_trace x segments per launch / the average launch time during the timed steps, measured on the
+device clock inside the kernel (first workgroup start to last workgroup end; agrees with rocprofv3's
+kernel-trace durations).  HIP events on the launching stream are reported beside it: with several
+iterations in flight they also count the time a launch waits behind the other iterations' kernels.
 """
 from __future__ import annotations
 
@@ -33,7 +35,8 @@ sys.path.insert(0, ROOT)
 # kdpt_trace_iterations keeps `--pipeline` iterations in flight on their own HIP streams plus one
 # accumulation stream; HIP's default of 4 hardware queues per process would make some of them share
 # a queue (and serialise), so ask for 8 before the runtime initialises.
-os.environ.setdefault("GPU_MAX_HW_QUEUES", "8")
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -127,15 +130,19 @@ def main():
     dt = time.perf_counter() - t0
     st1 = pt.stats()
     seg = st1.total_segments - st0.total_segments
-    kernel_ms = st1.intersect_ms_total - st0.intersect_ms_total
-    launches = st1.intersect_launches_total - st0.intersect_launches_total
+    ev_ms = st1.intersect_ms_total - st0.intersect_ms_total  # HIP events around each intersect launch
+    ev_launches = st1.intersect_launches_total - st0.intersect_launches_total
+    kernel_ms = st1.intersect_device_ms_total - st0.intersect_device_ms_total  # device clock, per launch
+    launches = st1.intersect_device_launches_total - st0.intersect_device_launches_total
     if dist:
-        t = torch.tensor([dt, float(seg), kernel_ms, float(launches)], dtype=torch.float64, device=f"cuda:{local}")
+        t = torch.tensor([dt, float(seg), kernel_ms, float(launches), ev_ms, float(ev_launches)], dtype=torch.float64,
+                         device=f"cuda:{local}")
         tmax = t[0:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t[1:].clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         dt, seg, kernel_ms, launches = float(tmax[0]), int(tsum[0]), float(tsum[1]), int(tsum[2])
+        ev_ms, ev_launches = float(tsum[3]), int(tsum[4])
     if rank != 0:
         pt.close()
         if dist:
@@ -179,12 +186,17 @@ def main():
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                      "kernel": "k_trace (intersect: analytic geoms + KD traversal)",
                      "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
+                     "avg_launch_ms_events": round(ev_ms / max(1, ev_launches), 5),
                      "aggregate_GBps": round(per_seg_bytes * seg / dt / 1e9, 2),
                      "bytes_per_segment": round(per_seg_bytes, 2),
                      "per_segment_counts": {"aabb": round(aabb / count_seg, 4), "tri": round(tri / count_seg, 4),
                                             "hit": round(hit / count_seg, 5)}},
         "reference_980m_intersect_ms_per_iter": 79.4,
         "intersect_ms_per_iter": round(kernel_ms / (args.steps * world), 4),
+        "timing_note": "avg_launch_ms: intersect launches on the device clock (s_memrealtime, first block start to "
+                       "last block end), comparable with rocprofv3 kernel-trace durations; avg_launch_ms_events: HIP "
+                       "events on the launching stream, which also count queueing behind the other in-flight "
+                       "iterations' kernels",
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)

@@ -158,6 +158,10 @@ typedef struct kdpt_stats {
     long long total_segments;    /* since create/reset */
     double intersect_ms_total;   /* testing_mode: intersect-kernel time summed over launches since reset */
     long long intersect_launches_total; /* ... and the number of those launches */
+    double intersect_device_ms_total;   /* intersect launches on the device clock (first block start to
+                                           last block end), summed since reset -- unlike the events,
+                                           not inflated by queueing when iterations overlap */
+    long long intersect_device_launches_total;
 } kdpt_stats;
 
 typedef struct kdpt_ctx kdpt_ctx;

@@ -73,13 +73,18 @@ __device__ inline unsigned int lane_prefix(unsigned long long mask) {
 // ---------------------------------------------------------------------------
 __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int traceDepth, PathBuf out,
                                                   float focalLength, float dofAngle, int antialias, int* counts,
-                                                  int ncounts, int* work, int nwork) {
+                                                  int ncounts, int* work, int nwork,
+                                                  unsigned long long* trace_t) {
   const int W = cam.resolution[0], H = cam.resolution[1];
   const int index = blockIdx.x * blockDim.x + threadIdx.x;
   if (index == 0) {
     counts[0] = W * H;
     for (int k = 1; k < ncounts; k++) counts[k] = 0;
-    for (int k = 0; k < nwork; k++) work[k] = 0;
+    for (int k = 0; k < nwork; k++) {
+      work[k] = 0;
+      trace_t[2 * k] = ~0ull;
+      trace_t[2 * k + 1] = 0ull;
+    }
   }
   if (index >= W * H) return;
   const int x = index % W, y = index / W;
@@ -151,6 +156,7 @@ struct TraceArgs {
   int* work;  // [cap] chunk counters, zeroed by k_gen_rays
   int depth;
   Counters* counters;
+  unsigned long long* trace_t;  // [2 * cap] first block start / last block end (s_memrealtime)
 };
 
 __device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, WaveLeafLDS* W,
@@ -194,6 +200,14 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
   const int lane = threadIdx.x & 63;
   WaveLeafLDS* W = &s_leaf[threadIdx.x >> 6];
   if (COUNT && lane < PROF_SLOTS) W->prof[lane] = 0;
+  // launch duration on the device clock (first block start .. last block end); the HIP events around
+  // the launch also count time spent queued behind other streams' kernels when iterations overlap
+  __shared__ int s_waves_done;
+  if (threadIdx.x == 0) {
+    s_waves_done = 0;
+    atomicMin(&A.trace_t[2 * A.depth], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  }
+  __syncthreads();
   int* work = A.work + A.depth;
   const unsigned long long rt0 = COUNT ? __builtin_amdgcn_s_memrealtime() : 0ull;
   // First chunk: the wave's own index (no atomic -- thousands of waves start at once);
@@ -228,6 +242,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
         const unsigned long long us10 = (__builtin_amdgcn_s_memrealtime() - rt0) / 1000;  // 100 MHz ticks
         atomicAdd(&A.counters->life[us10 < 63 ? us10 : 63], 1ull);
       }
+      if (lane == 0 && atomicAdd(&s_waves_done, 1) == TRACE_BLOCK / 64 - 1)
+        atomicMax(&A.trace_t[2 * A.depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
       break;
     }
     const unsigned long long t_k0 = COUNT ? __builtin_readcyclecounter() : 0ull;
@@ -324,6 +340,8 @@ struct ShadeArgs {
   int ntiles;
   int nkeys;
   unsigned long long* total_segments;  // running sum of paths launched into the intersect kernel
+  const unsigned long long* trace_t;   // this bounce's intersect launch record (see TraceArgs)
+  unsigned long long* trace_total;     // [2]: summed launch ticks, launches
 };
 
 template <bool HYBRID, bool COMPACT, bool SORT>
@@ -332,7 +350,14 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   const int tile = blockIdx.x;
   if (tile * TILE >= n) return;  // uniform per block
   const int i = tile * TILE + threadIdx.x;
-  if (i == 0) atomicAdd(A.total_segments, (unsigned long long)n);
+  if (i == 0) {
+    atomicAdd(A.total_segments, (unsigned long long)n);
+    const unsigned long long t0 = A.trace_t[2 * A.depth], t1 = A.trace_t[2 * A.depth + 1];
+    if (t1 > t0) {  // the intersect launch before this one on the stream ran (n > 0)
+      atomicAdd(&A.trace_total[0], t1 - t0);
+      atomicAdd(&A.trace_total[1], 1ull);
+    }
+  }
   __shared__ int s_hist[MAX_KEYS];
   __shared__ int s_khist[TRACE_KEYS];
   if (SORT) {
@@ -629,6 +654,9 @@ struct kdpt_ctx {
   Counters* counters = nullptr;
   Counters last_profile{};
   unsigned long long* total_segments = nullptr;  // device running total (async use)
+  unsigned long long* trace_t = nullptr;         // per-bounce intersect launch record (per slot)
+  unsigned long long* trace_total = nullptr;     // [2] device-clock intersect ticks, launches (shared)
+  double wall_khz = 100000.0;                    // s_memrealtime frequency
   int* h_counts = nullptr;  // pinned
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
   std::vector<hipEvent_t> bounce_ev;
@@ -701,6 +729,8 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
   }
   // counts[0..cap+1]: live paths per bounce (rewritten every iteration); counts[cap+2]: fault flag;
   // counts[cap+3 ..]: work counters of the persistent intersect kernel
+  if ((rc = dalloc(c, &c->trace_t, 2 * (size_t)c->cap))) return rc;
+  HIP_TRY(hipMemset(c->trace_t, 0, sizeof(unsigned long long) * 2 * c->cap));
   if ((rc = dalloc(c, &c->counts, 2 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->perm, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->tile_kcounts, (size_t)TRACE_KEYS * c->ntiles)) ||
@@ -748,6 +778,8 @@ int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
   for (int k = 0; k < 3; k++) c->chunk_width[k] = p->chunk_width[k];
   c->counters = p->counters;
   c->total_segments = p->total_segments;
+  c->trace_total = p->trace_total;
+  c->wall_khz = p->wall_khz;
   c->sync_debug = p->sync_debug;
   int rc;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
@@ -1159,7 +1191,14 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   } else if ((rc = dalloc(c, &c->image, 3 * (size_t)c->npix))) {
     return bail(rc);
   }
-  if ((rc = dalloc(c, &c->counters, 1)) || (rc = dalloc(c, &c->total_segments, 1))) return bail(rc);
+  if ((rc = dalloc(c, &c->counters, 1)) || (rc = dalloc(c, &c->total_segments, 1)) ||
+      (rc = dalloc(c, &c->trace_total, 2)))
+    return bail(rc);
+  {
+    int khz = 0;
+    if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
+      c->wall_khz = khz;
+  }
   {
     const char* e = getenv("KDPT_SYNC_DEBUG");
     c->sync_debug = e && e[0] == '1';
@@ -1192,6 +1231,7 @@ int kdpt_reset(kdpt_ctx* c) {
   c->intersect_launches_total = 0;
   HIP_TRY(hipMemsetAsync(c->image, 0, sizeof(float) * 3 * (size_t)c->npix, c->stream));
   HIP_TRY(hipMemsetAsync(c->total_segments, 0, sizeof(unsigned long long), c->stream));
+  HIP_TRY(hipMemsetAsync(c->trace_total, 0, 2 * sizeof(unsigned long long), c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   memset(&c->stats, 0, sizeof c->stats);
   return KDPT_OK;
@@ -1327,9 +1367,12 @@ int kdpt_write_pbo(kdpt_ctx* c, int iter, uint8_t* rgba) {
 int kdpt_get_stats(kdpt_ctx* c, kdpt_stats* st) {
   if (!c || !st) return fail(KDPT_ERR_ARG, "null arg");
   HIP_TRY(hipSetDevice(c->device));
-  unsigned long long tot = 0;
+  unsigned long long tot = 0, tt[2] = {0, 0};
   HIP_TRY(hipMemcpyAsync(&tot, c->total_segments, sizeof tot, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipMemcpyAsync(tt, c->trace_total, sizeof tt, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  c->stats.intersect_device_ms_total = (double)tt[0] / c->wall_khz;
+  c->stats.intersect_device_launches_total = (long long)tt[1];
   c->stats.total_segments = (long long)tot;
   c->stats.intersect_ms_total = c->intersect_ms_total;
   c->stats.intersect_launches_total = c->intersect_launches_total;
@@ -1523,7 +1566,7 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
   c->cur = 0;
   hipLaunchKernelGGL(k_gen_rays, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->cam, gen_iter,
                      c->traceDepth, c->buf[0], c->opt.focal_length, c->opt.dof_angle, c->opt.antialias, c->counts,
-                     c->cap + 2, c->work, c->cap);
+                     c->cap + 2, c->work, c->cap, c->trace_t);
   HIP_TRY(hipGetLastError());
   const bool compact = c->opt.compaction != 0;
   const bool sort = (iter == 2);
@@ -1542,6 +1585,7 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
     t.work = c->work;
     t.depth = depth;
     t.counters = c->counters;
+    t.trace_t = c->trace_t;
     std::vector<hipEvent_t>& bev = c->rec_ev ? *c->rec_ev : c->bounce_ev;
     if (c->opt.testing_mode) HIP_TRY(hipEventRecord(bev[2 * depth], c->stream));
     launch_trace(c, t, count);
@@ -1568,6 +1612,8 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
     a.ntiles = c->ntiles;
     a.nkeys = c->nkeys;
     a.total_segments = c->total_segments;
+    a.trace_t = c->trace_t;
+    a.trace_total = c->trace_total;
     if (c->opt.short_stack) launch_shade_h<true>(c, a, compact, sort);
     else launch_shade_h<false>(c, a, compact, sort);
     HIP_TRY(hipGetLastError());

@@ -84,7 +84,8 @@ class Stats(C.Structure):
     _fields_ = [("segments", C.c_longlong), ("seg_per_bounce", C.c_longlong * 32), ("bounces", C.c_int),
                 ("iterations", C.c_int), ("ms_last_iteration", C.c_float), ("ms_intersect", C.c_float),
                 ("total_segments", C.c_longlong), ("intersect_ms_total", C.c_double),
-                ("intersect_launches_total", C.c_longlong)]
+                ("intersect_launches_total", C.c_longlong), ("intersect_device_ms_total", C.c_double),
+                ("intersect_device_launches_total", C.c_longlong)]
 
 
 class SceneDesc(C.Structure):
