@@ -54,8 +54,9 @@ def parse():
     ap.add_argument("--bare", action="store_true", help="traverseKDbare instead of the short-stack hybrid")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--pipeline", type=int, default=3,
-                    help="iterations in flight (kdpt_trace_iterations; bit-identical to one at a time)")
+    ap.add_argument("--pipeline", type=int, default=2,
+                    help="batches in flight (kdpt_trace_iterations; bit-identical to one at a time)")
+    ap.add_argument("--batch", type=int, default=2, help="iterations sharing each intersect launch (<= 4)")
     return ap.parse_args()
 
 
@@ -108,7 +109,7 @@ def main():
 
     # warmup (iterations disjoint from the timed ones); iteration 2's extra sort lands here
     if args.warmup:
-        pt.trace_iterations(global_iter(0), args.warmup, stride=world, pipeline=args.pipeline)
+        pt.trace_iterations(global_iter(0), args.warmup, stride=world, pipeline=args.pipeline, batch=args.batch)
         pt.synchronize()
     # roofline counters from one untimed counting iteration of the timed range
     aabb, tri, hit = pt.count_iteration(global_iter(args.warmup))
@@ -120,7 +121,8 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    pt.trace_iterations(global_iter(args.warmup), args.steps, stride=world, pipeline=args.pipeline)
+    pt.trace_iterations(global_iter(args.warmup), args.steps, stride=world, pipeline=args.pipeline,
+                        batch=args.batch)
     pt.synchronize()
     reduce_image(accum, dist)  # spp shards -> one framebuffer (the only exchange step)
     torch.cuda.synchronize()
@@ -175,7 +177,7 @@ def main():
         "data": "synthetic camera rays over the reference's own scene assets (cornell.txt + dragon_5.obj, "
                 "parsed fixtures under tests/golden); deterministic RNG seeded by iteration",
         "config": {"workload": f"{args.scene}.txt + {args.mesh}.obj, {W}x{H}, depth {args.depth}, 1 spp per step "
-                               f"per GPU ({args.pipeline} iterations in flight), "
+                               f"per GPU ({args.pipeline} x {args.batch} iterations in flight), "
                                + ("short-stack hybrid KD traversal" if not args.bare else "bare traversal"),
                    "scene": args.scene, "mesh": args.mesh, "resolution": [W, H], "depth": args.depth,
                    "kd_nodes": sd.view.num_nodes, "kd_tri_refs": sd.view.num_tris,

@@ -567,310 +567,343 @@ __device__ inline float tri_hit_t(const DevScene& S, int i, f3 o, f3 d, float bx
   return distance(o, hit);
 }
 
-template <bool HYBRID, bool COUNT, typename NodeSrc, typename ClusterSrc>
-__device__ int traverseKD_wave(const DevScene& S, const NodeSrc& nodes, const ClusterSrc& clusters, const Ray& ray,
-                               bool active, Hit& h, int material_size, TraverseCounters& cnt, WaveLeafLDS* W) {
-  int objTri = -1;  // returned: the triangle whose hit record won (valid when h.obj_intersect)
+// One lane's ray and traversal state: exactly traverseKD's locals, kept across trace_phase calls so
+// that the intersect kernel can give a lane a new ray whenever its previous one is finished.
+struct WaveRay {
+  f3 o, d, invdir;
+  int cur, L;
+  uint32_t cb, ps, g;
+  bool rootv, sink, hitGeom, done, fault;
+  float bz;
+  int guard;
+  Hit h;
+  int objTri;  // the triangle whose hit record won (valid when h.obj_intersect)
+};
+
+// Start a ray: t_min / hit_geom_index come from the analytic geoms (k_geoms), tested first as in
+// pathTraceOneBounceKDbare.
+__device__ inline void wave_ray_start(const DevScene& S, WaveRay& R, f3 o, f3 d, float t_geom, int geom,
+                                      WaveLeafLDS* W) {
   const int lane = threadIdx.x & 63;
-  const f3 o = ray.origin, d = ray.direction;
+  R.o = o;
+  R.d = d;
+  R.invdir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  R.cur = S.root;
+  R.L = 0;
+  R.cb = R.ps = R.g = 0;
+  R.rootv = R.sink = R.hitGeom = R.done = R.fault = false;
+  R.bz = FLT_MAXV;
+  R.guard = 0;
+  R.h.t_min = t_geom;
+  R.h.hit_geom_index = geom;
+  R.h.obj_intersect = false;
+  R.h.objMaterialIdx = -1;
+  R.h.ip = mk3(0, 0, 0);
+  R.h.normal = mk3(0, 0, 0);
+  R.objTri = -1;
   W->od[lane] = make_float4(o.x, o.y, o.z, d.x);
   W->dd[lane] = make_float2(d.y, d.z);
-  const f3 invdir = active ? mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z) : mk3(0, 0, 0);
-  int cur = S.root, L = 0;
-  uint32_t cb = 0, ps = 0, g = 0;
-  bool rootv = false, sink = false, hitGeom = false;
-  bool done = !active;
-  float dist = -1.0f, bz = FLT_MAXV;
-  int guard = 0;  // node steps of this ray; > S.trip_limit means a corrupt tree: stop and flag
-  int phases = 0;  // leaf phases of this wave, bounded the same way
-  bool fault = false;
-  // IEEE min/max AABB slabs are exact unless some invdir component is infinite (wave-uniform)
-  const bool fastAABB = __all(!active || (fabsf(invdir.x) < FLT_INFV && fabsf(invdir.y) < FLT_INFV &&
-                                          fabsf(invdir.z) < FLT_INFV));
+}
+
+// One node phase and one leaf phase of traverseKD for every lane of the wave with an unfinished ray
+// (R.done false); lanes finish by setting R.done.  fastAABB must be wave-uniform (every active lane's
+// invdir finite).
+template <bool HYBRID, bool COUNT, typename NodeSrc, typename ClusterSrc>
+__device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const ClusterSrc& clusters, WaveRay& R,
+                            bool fastAABB, int material_size, TraverseCounters& cnt, WaveLeafLDS* W) {
+  const int lane = threadIdx.x & 63;
+  const f3 o = R.o, d = R.d, invdir = R.invdir;
+  int& cur = R.cur;
+  int& L = R.L;
+  uint32_t& cb = R.cb;
+  uint32_t& ps = R.ps;
+  uint32_t& g = R.g;
+  bool& rootv = R.rootv;
+  bool& sink = R.sink;
+  bool& hitGeom = R.hitGeom;
+  bool& done = R.done;
+  bool& fault = R.fault;
+  float& bz = R.bz;
+  int& guard = R.guard;
+  Hit& h = R.h;
+  int& objTri = R.objTri;
+  // ---------------- node phase ----------------
+  bool leaf = false;
+  int lstart = 0, lsize = 0, lparent = -1, lnode = 0;
+  bool lfirst = true;
+  int trips = 0;
+  if (COUNT) prof_lap(W, -1);
+  // One trip = one step of the reference's loop for every lane still walking nodes.  The
+  // body runs for the whole wave and commits by selects on `walk`, and the per-lane flags
+  // live in one register, so a trip carries no exec-mask bookkeeping.  Exact for a
+  // validated tree (only the root has parentID == -1): at the root `up` ends the walk (the
+  // reference exits before or after its test, or climbs to -1), so hitGeom only feeds the
+  // AABB count.
+  enum : uint32_t { F_ROOTV = 1, F_SINK = 2, F_HITGEOM = 4, F_DONE = 8, F_LEAF = 16, F_LFIRST = 32, F_FAULT = 64 };
+  uint32_t fl = (rootv ? F_ROOTV : 0u) | (sink ? F_SINK : 0u) | (hitGeom ? F_HITGEOM : 0u) | (done ? F_DONE : 0u) |
+                F_LFIRST;
   while (true) {
-    // ---------------- node phase ----------------
-    bool leaf = false;
-    int lstart = 0, lsize = 0, lparent = -1, lnode = 0;
-    bool lfirst = true;
-    int trips = 0;
-    if (COUNT) prof_lap(W, -1);
-    // One trip = one step of the reference's loop for every lane still walking nodes.  The
-    // body runs for the whole wave and commits by selects on `walk`, and the per-lane flags
-    // live in one register, so a trip carries no exec-mask bookkeeping.  Exact for a
-    // validated tree (only the root has parentID == -1): at the root `up` ends the walk (the
-    // reference exits before or after its test, or climbs to -1), so hitGeom only feeds the
-    // AABB count.
-    enum : uint32_t { F_ROOTV = 1, F_SINK = 2, F_HITGEOM = 4, F_DONE = 8, F_LEAF = 16, F_LFIRST = 32, F_FAULT = 64 };
-    uint32_t fl = (rootv ? F_ROOTV : 0u) | (sink ? F_SINK : 0u) | (hitGeom ? F_HITGEOM : 0u) | (done ? F_DONE : 0u) |
-                  F_LFIRST;
-    while (true) {
-      const bool walk = (fl & (F_DONE | F_LEAF)) == 0u;
-      const unsigned long long wmask = __ballot(walk);
-      if (!wmask) break;
-      // Few lanes still walking and many waiting on leaves: test those leaves now; the walkers keep
-      // their state and resume in the next node phase (their own sequence of steps is unchanged).
-      if (__popcll(wmask) <= S.early_walk && __popcll(__ballot((fl & F_LEAF) != 0u)) >= S.early_leaf) break;
-      if (COUNT) trips += walk ? 1 : 0;
-      const NodeRec nd = nodes(cur < 0 ? 0 : cur);
-      const int left = nd.left, right = nd.right;
-      const uint32_t Lu = (uint32_t)L;
-      const uint32_t vb = (2u * Lu - 2u + ((ps >> ((Lu - 1u) & 31u)) & 1u)) & 31u;  // own flag (L > 0)
-      const bool curVis = (L == 0) ? ((fl & F_ROOTV) != 0u) : (((cb >> vb) & 1u) != 0u);
-      const bool isRoot = cur == S.root;
-      float dd;
-      const bool hg = fastAABB ? intersectAABB_fast(o, invdir, nd.b0, nd.b1, dd)
-                               : intersectAABB(o, invdir, nd.b0, nd.b1, dd);
-      const bool up = curVis || !hg || dd > bz;
-      const bool leftFirst = HYBRID ? (comp(d, nd.axis) > 0.0f) : true;
-      const uint32_t fside = leftFirst ? 0u : 1u;
-      const uint32_t cl = (cb >> ((2u * Lu) & 31u)) & 3u;  // child flags of this level
-      const int first = leftFirst ? left : right, second = leftFirst ? right : left;
-      const bool takeFirst = first != -1 && !((cl >> fside) & 1u);
-      const bool takeSecond = second != -1 && !((cl >> (fside ^ 1u)) & 1u);
-      const bool descend = !up && (takeFirst || takeSecond);
-      const uint32_t nside = takeFirst ? fside : (fside ^ 1u);
-      const bool lf = !up && !descend && nd.triSize > 0;
-      // "Mark and stay" on a node without triangles is always followed by a trip on the same
-      // node that finds it visited and climbs (same box, so same hitGeom): do both now.
-      const bool stay = !up && !descend && !lf;
-      const bool climb = up || stay;
-      if (COUNT && walk) cnt.aabb += (isRoot && curVis && !(fl & F_HITGEOM)) ? 0u : (stay ? 2u : 1u);
-      // nodeIDs[ID] = true unless descending; nodeIDs[left] = nodeIDs[right] = true when climbing
-      uint32_t ncb = cb | ((!descend && L > 0) ? (1u << vb) : 0u);
-      ncb |= climb ? ((left != -1 ? 1u : 0u) | (right != -1 ? 2u : 0u)) << ((2u * Lu) & 31u) : 0u;
-      const uint32_t dcb = (ncb & ~(3u << ((2u * Lu + 2u) & 31u))) | ((L == 0 && nside == 0u) ? (g << 2) : 0u);
-      const bool runaway = guard >= S.trip_limit;
-      uint32_t nfl = fl & ~(F_HITGEOM | F_LFIRST);
-      nfl |= (!descend && L == 0) ? F_ROOTV : 0u;
-      nfl |= (climb && (left == -1 || right == -1)) ? F_SINK : 0u;
-      nfl |= hg ? F_HITGEOM : 0u;
-      nfl |= ((isRoot && climb) || runaway) ? F_DONE : 0u;
-      nfl |= runaway ? F_FAULT : 0u;
-      nfl |= lf ? F_LEAF : 0u;
-      nfl |= leftFirst ? F_LFIRST : 0u;
-      if (walk) {  // commit (selects)
-        cb = descend ? dcb : ncb;
-        ps = descend ? ((ps & ~(1u << (Lu & 31u))) | (nside << (Lu & 31u))) : ps;
-        cur = climb ? nd.parent : (descend ? (takeFirst ? first : second) : cur);
-        L += descend ? 1 : (climb ? -1 : 0);
-        guard++;
-        fl = nfl;
-        lstart = nd.triStart;
-        lsize = nd.triSize;
-        lparent = nd.parent;
-        lnode = cur;
-      }
+    const bool walk = (fl & (F_DONE | F_LEAF)) == 0u;
+    const unsigned long long wmask = __ballot(walk);
+    if (!wmask) break;
+    // Few lanes still walking and many waiting on leaves: test those leaves now; the walkers keep
+    // their state and resume in the next node phase (their own sequence of steps is unchanged).
+    if (__popcll(wmask) <= S.early_walk && __popcll(__ballot((fl & F_LEAF) != 0u)) >= S.early_leaf) break;
+    if (COUNT) trips += walk ? 1 : 0;
+    const NodeRec nd = nodes(cur < 0 ? 0 : cur);
+    const int left = nd.left, right = nd.right;
+    const uint32_t Lu = (uint32_t)L;
+    const uint32_t vb = (2u * Lu - 2u + ((ps >> ((Lu - 1u) & 31u)) & 1u)) & 31u;  // own flag (L > 0)
+    const bool curVis = (L == 0) ? ((fl & F_ROOTV) != 0u) : (((cb >> vb) & 1u) != 0u);
+    const bool isRoot = cur == S.root;
+    float dd;
+    const bool hg = fastAABB ? intersectAABB_fast(o, invdir, nd.b0, nd.b1, dd)
+                             : intersectAABB(o, invdir, nd.b0, nd.b1, dd);
+    const bool up = curVis || !hg || dd > bz;
+    const bool leftFirst = HYBRID ? (comp(d, nd.axis) > 0.0f) : true;
+    const uint32_t fside = leftFirst ? 0u : 1u;
+    const uint32_t cl = (cb >> ((2u * Lu) & 31u)) & 3u;  // child flags of this level
+    const int first = leftFirst ? left : right, second = leftFirst ? right : left;
+    const bool takeFirst = first != -1 && !((cl >> fside) & 1u);
+    const bool takeSecond = second != -1 && !((cl >> (fside ^ 1u)) & 1u);
+    const bool descend = !up && (takeFirst || takeSecond);
+    const uint32_t nside = takeFirst ? fside : (fside ^ 1u);
+    const bool lf = !up && !descend && nd.triSize > 0;
+    // "Mark and stay" on a node without triangles is always followed by a trip on the same
+    // node that finds it visited and climbs (same box, so same hitGeom): do both now.
+    const bool stay = !up && !descend && !lf;
+    const bool climb = up || stay;
+    if (COUNT && walk) cnt.aabb += (isRoot && curVis && !(fl & F_HITGEOM)) ? 0u : (stay ? 2u : 1u);
+    // nodeIDs[ID] = true unless descending; nodeIDs[left] = nodeIDs[right] = true when climbing
+    uint32_t ncb = cb | ((!descend && L > 0) ? (1u << vb) : 0u);
+    ncb |= climb ? ((left != -1 ? 1u : 0u) | (right != -1 ? 2u : 0u)) << ((2u * Lu) & 31u) : 0u;
+    const uint32_t dcb = (ncb & ~(3u << ((2u * Lu + 2u) & 31u))) | ((L == 0 && nside == 0u) ? (g << 2) : 0u);
+    const bool runaway = guard >= S.trip_limit;
+    uint32_t nfl = fl & ~(F_HITGEOM | F_LFIRST);
+    nfl |= (!descend && L == 0) ? F_ROOTV : 0u;
+    nfl |= (climb && (left == -1 || right == -1)) ? F_SINK : 0u;
+    nfl |= hg ? F_HITGEOM : 0u;
+    nfl |= ((isRoot && climb) || runaway) ? F_DONE : 0u;
+    nfl |= runaway ? F_FAULT : 0u;
+    nfl |= lf ? F_LEAF : 0u;
+    nfl |= leftFirst ? F_LFIRST : 0u;
+    if (walk) {  // commit (selects)
+      cb = descend ? dcb : ncb;
+      ps = descend ? ((ps & ~(1u << (Lu & 31u))) | (nside << (Lu & 31u))) : ps;
+      cur = climb ? nd.parent : (descend ? (takeFirst ? first : second) : cur);
+      L += descend ? 1 : (climb ? -1 : 0);
+      guard++;
+      fl = nfl;
+      lstart = nd.triStart;
+      lsize = nd.triSize;
+      lparent = nd.parent;
+      lnode = cur;
     }
-    rootv = (fl & F_ROOTV) != 0u;
-    sink = (fl & F_SINK) != 0u;
-    hitGeom = (fl & F_HITGEOM) != 0u;
-    done = (fl & F_DONE) != 0u;
-    leaf = (fl & F_LEAF) != 0u;
-    lfirst = (fl & F_LFIRST) != 0u;
-    fault = fault || (fl & F_FAULT) != 0u;
-    if (COUNT) {
-      prof_lap(W, PROF_NODE_CYC);
-      for (int off = 32; off > 0; off >>= 1) trips = max(trips, __shfl_xor(trips, off));
-      prof_add(W, PROF_NODE_TRIPS, (unsigned long long)trips);  // wave-level trips = the slowest lane's
-    }
-    if (__any(fault) && lane == 0) atomicOr(S.fault, 1);
-    if (!__any(leaf)) break;
-    if (++phases > S.trip_limit) {  // uniform; unreachable for a validated tree
-      if (lane == 0) atomicOr(S.fault, 2);
-      break;
-    }
-    // ---------------- leaf phase (wave-cooperative) ----------------
-    // per lane results of this phase
-    int r_pass = 0;          // 0 = none, else tri + 1 of the last u/v pass
-    float r_bz = 0.0f;
-    int r_lasthit = -1, r_nhit = 0;
-    unsigned long long r_best = ~0ull;
-    // (a) big leaves: the whole wave sweeps one leaf at a time with a uniform ray
-    const bool big = leaf && lsize >= BIG_LEAF;
-    unsigned long long bigmask = __ballot(big);
-    while (bigmask) {
-      // One big leaf at a time, the whole wave on it with that lane's ray: clusters whose box the
-      // ray's line misses are skipped (when every invdir is finite), the others tested 64 at a time.
-      // Recombination by ORIGINAL index: last u/v pass = max index, last hit = max, best = min (t, index).
-      const int j = __builtin_ctzll(bigmask);
-      bigmask &= bigmask - 1;
-      const int jfirst = __builtin_amdgcn_readfirstlane(
-          NodeSrc::kLeafHoldsCluster ? __shfl(lstart, j) : S.leaf_cl[__shfl(lnode, j)].x);
-      const int jcount = (__builtin_amdgcn_readfirstlane(__shfl(lsize, j)) + 63) >> 6;
-      const f3 jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
-      const f3 jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
-      const f3 jinv = mk3(__shfl(invdir.x, j), __shfl(invdir.y, j), __shfl(invdir.z, j));
-      const int2 cr = make_int2(jfirst, jcount);
-      unsigned long long u_pass = 0ull, u_best = ~0ull;
-      int u_lasthit = -1, u_nhit = 0;
-      for (int cb0 = 0; cb0 < cr.y; cb0 += 64) {
-       // lane k culls cluster cb0 + k: one parallel pass over the boxes, then only the survivors
-       const int ck = cr.x + cb0 + lane;
-       const bool cv = cb0 + lane < cr.y;
-       const int cq = cv ? ck : cr.x;
-       unsigned long long cmask =
-           __ballot(cv && (!fastAABB || cluster_may_pass(clusters.lo_of(cq), clusters.hi_of(cq), jo, jinv)));
-       while (cmask) {
-        const int c = cr.x + cb0 + __builtin_ctzll(cmask);
-        cmask &= cmask - 1;
-        if (COUNT) prof_add(W, PROF_BIG_SWEEPS, 1);
-        const int2 ci = S.cl_info[c];
-        const bool in = lane < ci.y;
-        const int ct = ci.x + (in ? lane : 0);
-        const TriData T{S.c_v0[ct], S.c_e1[ct], S.c_e2[ct]};
-        const int orig = fbits(T.e1.w);
-        float bx = 0, by = 0, bzk = 0;
-        const int r = in ? tri_test_v(T, jo, jd, bx, by, bzk) : 0;
-        if (__ballot(r >= 1)) {
-          const unsigned long long pk =
-              r >= 1 ? ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk) : 0ull;
-          const unsigned long long wm = wave_max_u64(pk);
-          u_pass = wm > u_pass ? wm : u_pass;
-          const unsigned long long m2 = __ballot(r == 2);
-          if (m2) {
-            u_nhit += __builtin_popcountll(m2);
-            u_lasthit = max(u_lasthit, wave_max_i32(r == 2 ? orig : -1));
-            unsigned long long key = ~0ull;
-            if (r == 2) {
-              f3 hp, nn;
-              const float t = tri_hit_t<HYBRID>(S, orig, jo, jd, bx, by, bzk, hp, nn);
-              if (t > 0.0f) key = ((unsigned long long)f2u(t) << 32) | (unsigned int)orig;
-            }
-            const unsigned long long wb = wave_min_u64(key);
-            u_best = wb < u_best ? wb : u_best;
+  }
+  rootv = (fl & F_ROOTV) != 0u;
+  sink = (fl & F_SINK) != 0u;
+  hitGeom = (fl & F_HITGEOM) != 0u;
+  done = (fl & F_DONE) != 0u;
+  leaf = (fl & F_LEAF) != 0u;
+  lfirst = (fl & F_LFIRST) != 0u;
+  fault = fault || (fl & F_FAULT) != 0u;
+  if (COUNT) {
+    prof_lap(W, PROF_NODE_CYC);
+    for (int off = 32; off > 0; off >>= 1) trips = max(trips, __shfl_xor(trips, off));
+    prof_add(W, PROF_NODE_TRIPS, (unsigned long long)trips);  // wave-level trips = the slowest lane's
+  }
+  if (__any(fault) && lane == 0) atomicOr(S.fault, 1);
+  if (!__any(leaf)) return;
+  // ---------------- leaf phase (wave-cooperative) ----------------
+  // per lane results of this phase
+  int r_pass = 0;          // 0 = none, else tri + 1 of the last u/v pass
+  float r_bz = 0.0f;
+  int r_lasthit = -1, r_nhit = 0;
+  unsigned long long r_best = ~0ull;
+  // (a) big leaves: the whole wave sweeps one leaf at a time with a uniform ray
+  const bool big = leaf && lsize >= BIG_LEAF;
+  unsigned long long bigmask = __ballot(big);
+  while (bigmask) {
+    // One big leaf at a time, the whole wave on it with that lane's ray: clusters whose box the
+    // ray's line misses are skipped (when every invdir is finite), the others tested 64 at a time.
+    // Recombination by ORIGINAL index: last u/v pass = max index, last hit = max, best = min (t, index).
+    const int j = __builtin_ctzll(bigmask);
+    bigmask &= bigmask - 1;
+    const int jfirst = __builtin_amdgcn_readfirstlane(
+        NodeSrc::kLeafHoldsCluster ? __shfl(lstart, j) : S.leaf_cl[__shfl(lnode, j)].x);
+    const int jcount = (__builtin_amdgcn_readfirstlane(__shfl(lsize, j)) + 63) >> 6;
+    const f3 jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
+    const f3 jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
+    const f3 jinv = mk3(__shfl(invdir.x, j), __shfl(invdir.y, j), __shfl(invdir.z, j));
+    const int2 cr = make_int2(jfirst, jcount);
+    unsigned long long u_pass = 0ull, u_best = ~0ull;
+    int u_lasthit = -1, u_nhit = 0;
+    for (int cb0 = 0; cb0 < cr.y; cb0 += 64) {
+     // lane k culls cluster cb0 + k: one parallel pass over the boxes, then only the survivors
+     const int ck = cr.x + cb0 + lane;
+     const bool cv = cb0 + lane < cr.y;
+     const int cq = cv ? ck : cr.x;
+     unsigned long long cmask =
+         __ballot(cv && (!fastAABB || cluster_may_pass(clusters.lo_of(cq), clusters.hi_of(cq), jo, jinv)));
+     while (cmask) {
+      const int c = cr.x + cb0 + __builtin_ctzll(cmask);
+      cmask &= cmask - 1;
+      if (COUNT) prof_add(W, PROF_BIG_SWEEPS, 1);
+      const int2 ci = S.cl_info[c];
+      const bool in = lane < ci.y;
+      const int ct = ci.x + (in ? lane : 0);
+      const TriData T{S.c_v0[ct], S.c_e1[ct], S.c_e2[ct]};
+      const int orig = fbits(T.e1.w);
+      float bx = 0, by = 0, bzk = 0;
+      const int r = in ? tri_test_v(T, jo, jd, bx, by, bzk) : 0;
+      if (__ballot(r >= 1)) {
+        const unsigned long long pk =
+            r >= 1 ? ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk) : 0ull;
+        const unsigned long long wm = wave_max_u64(pk);
+        u_pass = wm > u_pass ? wm : u_pass;
+        const unsigned long long m2 = __ballot(r == 2);
+        if (m2) {
+          u_nhit += __builtin_popcountll(m2);
+          u_lasthit = max(u_lasthit, wave_max_i32(r == 2 ? orig : -1));
+          unsigned long long key = ~0ull;
+          if (r == 2) {
+            f3 hp, nn;
+            const float t = tri_hit_t<HYBRID>(S, orig, jo, jd, bx, by, bzk, hp, nn);
+            if (t > 0.0f) key = ((unsigned long long)f2u(t) << 32) | (unsigned int)orig;
           }
+          const unsigned long long wb = wave_min_u64(key);
+          u_best = wb < u_best ? wb : u_best;
         }
-       }
       }
-      if (lane == j) {
-        r_pass = (int)(u_pass >> 32);
-        r_bz = u2f((uint32_t)(u_pass & 0xffffffffu));
-        r_lasthit = u_lasthit;
-        r_nhit = u_nhit;
-        r_best = u_best;
-      }
+     }
     }
-    if (COUNT) prof_lap(W, PROF_BIG_CYC);
-    // (b) small leaves: all (ray, triangle) pairs spread over the 64 lanes
-    const int sz = (leaf && !big) ? lsize : 0;
-    if (__any(sz > 0)) {
-      if (COUNT) prof_add(W, PROF_SMALL_PHASES, 1);
-      int incl = sz;
+    if (lane == j) {
+      r_pass = (int)(u_pass >> 32);
+      r_bz = u2f((uint32_t)(u_pass & 0xffffffffu));
+      r_lasthit = u_lasthit;
+      r_nhit = u_nhit;
+      r_best = u_best;
+    }
+  }
+  if (COUNT) prof_lap(W, PROF_BIG_CYC);
+  // (b) small leaves: all (ray, triangle) pairs spread over the 64 lanes
+  const int sz = (leaf && !big) ? lsize : 0;
+  if (__any(sz > 0)) {
+    if (COUNT) prof_add(W, PROF_SMALL_PHASES, 1);
+    int incl = sz;
 #pragma unroll
-      for (int off = 1; off < 64; off <<= 1) {
-        const int y = __shfl_up(incl, off);
-        if (lane >= off) incl += y;
+    for (int off = 1; off < 64; off <<= 1) {
+      const int y = __shfl_up(incl, off);
+      if (lane >= off) incl += y;
+    }
+    const int P = __shfl(incl, 63);
+    W->pend[lane] = incl;
+    W->tbase[lane] = lstart - (incl - sz);
+    W->lastPass[lane] = 0ull;
+    W->lastHit[lane] = -1;
+    W->nhit[lane] = 0;
+    W->best[lane] = ~0ull;
+    wave_lds_sync();
+    if (COUNT) prof_add(W, PROF_SMALL_ROUNDS, (unsigned long long)((P + 63) / 64));
+    // pair pi -> owner lane (binary search over the inclusive ends) and triangle; the next
+    // round's pair is located and its triangle loaded while the current one is tested
+    auto owner_of = [&](int q) {
+      int lo = 0, hi = 63;
+#pragma unroll
+      for (int st = 0; st < 6; st++) {
+        const int mid = (lo + hi) >> 1;
+        if (W->pend[mid] > q) hi = mid; else lo = mid + 1;
       }
-      const int P = __shfl(incl, 63);
-      W->pend[lane] = incl;
-      W->tbase[lane] = lstart - (incl - sz);
-      W->lastPass[lane] = 0ull;
-      W->lastHit[lane] = -1;
-      W->nhit[lane] = 0;
-      W->best[lane] = ~0ull;
-      wave_lds_sync();
-      if (COUNT) prof_add(W, PROF_SMALL_ROUNDS, (unsigned long long)((P + 63) / 64));
-      // pair pi -> owner lane (binary search over the inclusive ends) and triangle; the next
-      // round's pair is located and its triangle loaded while the current one is tested
-      auto owner_of = [&](int q) {
-        int lo = 0, hi = 63;
-#pragma unroll
-        for (int st = 0; st < 6; st++) {
-          const int mid = (lo + hi) >> 1;
-          if (W->pend[mid] > q) hi = mid; else lo = mid + 1;
-        }
-        return lo;
-      };
-      int pi = lane;
-      int owner = 0, tri = 0;
-      TriData nxt{};
+      return lo;
+    };
+    int pi = lane;
+    int owner = 0, tri = 0;
+    TriData nxt{};
+    if (pi < P) {
+      owner = owner_of(pi);
+      tri = W->tbase[owner] + pi;
+      nxt = tri_load(S, tri);
+    }
+    while (pi < P) {
+      const TriData cur_t = nxt;
+      const int cowner = owner, ctri = tri;
+      pi += 64;
       if (pi < P) {
         owner = owner_of(pi);
         tri = W->tbase[owner] + pi;
         nxt = tri_load(S, tri);
       }
-      while (pi < P) {
-        const TriData cur_t = nxt;
-        const int cowner = owner, ctri = tri;
-        pi += 64;
-        if (pi < P) {
-          owner = owner_of(pi);
-          tri = W->tbase[owner] + pi;
-          nxt = tri_load(S, tri);
-        }
-        const float4 q0 = W->od[cowner];
-        const float2 q1 = W->dd[cowner];
-        const f3 oo = mk3(q0.x, q0.y, q0.z), dd = mk3(q0.w, q1.x, q1.y);
-        float bx, by, bzk;
-        const int r = tri_test_v(cur_t, oo, dd, bx, by, bzk);
-        if (r >= 1)
-          atomicMax(&W->lastPass[cowner], ((unsigned long long)(unsigned int)(ctri + 1) << 32) | f2u(bzk));
-        if (r == 2) {
-          atomicMax(&W->lastHit[cowner], ctri);
-          atomicAdd(&W->nhit[cowner], 1);
-          f3 hp, nn;
-          const float t = tri_hit_t<HYBRID>(S, ctri, oo, dd, bx, by, bzk, hp, nn);
-          if (t > 0.0f) atomicMin(&W->best[cowner], ((unsigned long long)f2u(t) << 32) | (unsigned int)ctri);
-        }
+      const float4 q0 = W->od[cowner];
+      const float2 q1 = W->dd[cowner];
+      const f3 oo = mk3(q0.x, q0.y, q0.z), dd = mk3(q0.w, q1.x, q1.y);
+      float bx, by, bzk;
+      const int r = tri_test_v(cur_t, oo, dd, bx, by, bzk);
+      if (r >= 1)
+        atomicMax(&W->lastPass[cowner], ((unsigned long long)(unsigned int)(ctri + 1) << 32) | f2u(bzk));
+      if (r == 2) {
+        atomicMax(&W->lastHit[cowner], ctri);
+        atomicAdd(&W->nhit[cowner], 1);
+        f3 hp, nn;
+        const float t = tri_hit_t<HYBRID>(S, ctri, oo, dd, bx, by, bzk, hp, nn);
+        if (t > 0.0f) atomicMin(&W->best[cowner], ((unsigned long long)f2u(t) << 32) | (unsigned int)ctri);
       }
-      wave_lds_sync();
-      if (sz > 0) {
-        const unsigned long long lp = W->lastPass[lane];
-        r_pass = (int)(lp >> 32);
-        r_bz = u2f((uint32_t)(lp & 0xffffffffu));
-        r_lasthit = W->lastHit[lane];
-        r_nhit = W->nhit[lane];
-        r_best = W->best[lane];
-      }
-      wave_lds_sync();  // the LDS slots are rewritten by the next leaf phase
     }
-    if (COUNT) prof_lap(W, PROF_SMALL_CYC);
-    if (leaf) {
-      if (COUNT) cnt.tri += lsize;
-      if (r_pass > 0) bz = r_bz;
-      const int nh = r_nhit;
-      if (nh > 0) {
-        if (COUNT) cnt.hit += nh;
-        h.objMaterialIdx = fbits(S.tv0[r_lasthit].w) + material_size - 1;
-        if (HYBRID) {
-          for (int rep = 0; rep < (nh > 1 ? 2 : 1); rep++) {
-            const bool parVis = (L == 0) ? sink
-                                : (L == 1 ? rootv
-                                          : (((cb >> (2 * (L - 2) + (int)((ps >> (L - 2)) & 1u))) & 1u) != 0u));
-            const int b = parVis ? 1 : 0;
-            int target = -1;
-            if (b < S.num_nodes) target = (b == 0) ? (lfirst ? S.n0_right : S.n0_left) : (lfirst ? S.n1_right : S.n1_left);
-            if (target == -1) sink = true;
-            else if (b == 0) cb |= 1u << (lfirst ? 1 : 0);
-            else {
-              const uint32_t bit = lfirst ? 1u : 0u;
-              if (L >= 1 && (ps & 1u) == 0u) cb |= 1u << (2 + bit);
-              else g |= 1u << bit;
-            }
-          }
-        }
-        if (r_best != ~0ull) {
-          const float tb = u2f((uint32_t)(r_best >> 32));
-          const int k = (int)(uint32_t)(r_best & 0xffffffffu);
-          if (h.t_min > tb) {  // tb is tri_hit_t's value for triangle k (the winner's point and
-            h.t_min = tb;        // normal are recomputed from k by the shading kernel)
-            h.hit_geom_index = S.obj_material_offsets[fbits(S.tv0[k].w)];
-            h.obj_intersect = true;
-            objTri = k;
-          }
-        }
-      }
-      // The reference's next trip finds the leaf visited and climbs (leaves have no children,
-      // validated: nodeIDs[-1] = true twice); do it here instead of in the node phase.
-      if (COUNT) cnt.aabb++;
-      sink = true;
-      done = cur == S.root;
-      cur = lparent;
-      L--;
+    wave_lds_sync();
+    if (sz > 0) {
+      const unsigned long long lp = W->lastPass[lane];
+      r_pass = (int)(lp >> 32);
+      r_bz = u2f((uint32_t)(lp & 0xffffffffu));
+      r_lasthit = W->lastHit[lane];
+      r_nhit = W->nhit[lane];
+      r_best = W->best[lane];
     }
-    if (COUNT) prof_lap(W, PROF_FINAL_CYC);
+    wave_lds_sync();  // the LDS slots are rewritten by the next leaf phase
   }
-  return objTri;
+  if (COUNT) prof_lap(W, PROF_SMALL_CYC);
+  if (leaf) {
+    if (COUNT) cnt.tri += lsize;
+    if (r_pass > 0) bz = r_bz;
+    const int nh = r_nhit;
+    if (nh > 0) {
+      if (COUNT) cnt.hit += nh;
+      h.objMaterialIdx = fbits(S.tv0[r_lasthit].w) + material_size - 1;
+      if (HYBRID) {
+        for (int rep = 0; rep < (nh > 1 ? 2 : 1); rep++) {
+          const bool parVis = (L == 0) ? sink
+                              : (L == 1 ? rootv
+                                        : (((cb >> (2 * (L - 2) + (int)((ps >> (L - 2)) & 1u))) & 1u) != 0u));
+          const int b = parVis ? 1 : 0;
+          int target = -1;
+          if (b < S.num_nodes) target = (b == 0) ? (lfirst ? S.n0_right : S.n0_left) : (lfirst ? S.n1_right : S.n1_left);
+          if (target == -1) sink = true;
+          else if (b == 0) cb |= 1u << (lfirst ? 1 : 0);
+          else {
+            const uint32_t bit = lfirst ? 1u : 0u;
+            if (L >= 1 && (ps & 1u) == 0u) cb |= 1u << (2 + bit);
+            else g |= 1u << bit;
+          }
+        }
+      }
+      if (r_best != ~0ull) {
+        const float tb = u2f((uint32_t)(r_best >> 32));
+        const int k = (int)(uint32_t)(r_best & 0xffffffffu);
+        if (h.t_min > tb) {  // tb is tri_hit_t's value for triangle k (the winner's point and
+          h.t_min = tb;        // normal are recomputed from k by the shading kernel)
+          h.hit_geom_index = S.obj_material_offsets[fbits(S.tv0[k].w)];
+          h.obj_intersect = true;
+          objTri = k;
+        }
+      }
+    }
+    // The reference's next trip finds the leaf visited and climbs (leaves have no children,
+    // validated: nodeIDs[-1] = true twice); do it here instead of in the node phase.
+    if (COUNT) cnt.aabb++;
+    sink = true;
+    done = cur == S.root;
+    cur = lparent;
+    L--;
+  }
+  if (COUNT) prof_lap(W, PROF_FINAL_CYC);
 }
 #endif  // HIP
 

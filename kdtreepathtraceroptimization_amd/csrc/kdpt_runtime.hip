@@ -142,18 +142,22 @@ __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int
 enum TreeMode { TREE_WIDE = 0, TREE_PACKED = 1, TREE_LDS = 2 };
 constexpr int TRACE_BLOCK = 1024;
 
-struct TraceArgs {
-  DevScene S;
+// Up to MAXB iterations (each its own path buffers) at the same bounce share one intersect launch:
+// more rays per launch keep the lanes of the persistent waves busy.
+constexpr int MAXB = 4;
+struct TraceIter {
   PathBuf paths;
-  const int* perm;  // trace order (chunk slot -> path index), or null for identity
-  // with perm: class starts in the trace order = koff[(k * keys_per_class) * ntiles_alloc], and the
-  // chunk width of each class (heavy classes get narrow chunks: their leaf work adds up per wave)
-  const int* koff;
-  int ntiles_alloc, keys_per_class, nclass;
-  int cw[3];
+  const int* perm;      // trace order (queue slot -> path index), or null for identity
+  const int2* geomhit;  // k_geoms' {t_min bits, geom index} per path
   int2* hits;
   const int* counts;
-  int* work;  // [cap] chunk counters, zeroed by k_gen_rays
+};
+
+struct TraceArgs {
+  DevScene S;
+  TraceIter it[MAXB];
+  int nb;
+  int* work;  // chunk counters, zeroed by k_gen_rays (of iteration 0 of the batch)
   int depth;
   Counters* counters;
   unsigned long long* trace_t;  // [2 * cap] first block start / last block end (s_memrealtime)
@@ -180,12 +184,57 @@ __device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, 
   }
 }
 
+// The analytic geoms of pathTraceOneBounceKDbare (tested before the KD tree; src/pathtrace.cu:1600-1640),
+// one lane per live path, consecutive paths per wave: {t_min bits, geom index} for k_trace.
+__global__ __launch_bounds__(256) void k_geoms(DevScene S, PathBuf paths, const int* counts, int depth,
+                                               int2* __restrict__ geomhit) {
+  const int n = counts[depth];
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  const float4 q1 = paths.p1[i];
+  if (fbits(paths.p2[i].w) <= 0) return;
+  const float4 q0 = paths.p0[i];
+  Ray ray;
+  ray.origin = mk3(q0.x, q0.y, q0.z);
+  ray.direction = mk3(q1.x, q1.y, q1.z);
+  ray.isinside = false;
+  ray.sdepth = q0.w;
+  float t_min = FLT_MAXV;
+  int hit = -1;
+  f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
+  float t = 0;
+  const f3 inv = mk3(1.0f / ray.direction.x, 1.0f / ray.direction.y, 1.0f / ray.direction.z);
+  const bool finite = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
+  for (int g = 0; g < S.num_geoms; g++) {
+    const DevGeom& G = S.geoms[g];
+    if (finite && !geom_may_hit(G, ray.origin, inv)) {
+      t = -1.0f;  // the exact test would miss
+    } else if (G.type == 1) {
+      t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
+    } else if (G.type == 0) {
+      t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+    }
+    if (t > 0.0f && t_min > t) {
+      t_min = t;
+      hit = g;
+    }
+  }
+  geomhit[i] = make_int2(fbits(t_min), hit);
+}
+
+// KD traversal of every live path.  Each lane holds one ray; whenever rays finish, the idle lanes take
+// the next paths of the bounce from a device counter, so a wave stays full until the bounce runs out
+// of paths (the per-ray algorithm is unchanged -- only which lane runs it, and when).
 template <bool HYBRID, bool COUNT, int MODE>
 __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
   extern __shared__ int4 s_tree[];
   __shared__ WaveLeafLDS s_leaf[TRACE_BLOCK / 64];
   const DevScene& S = A.S;
-  const int n = A.counts[A.depth];
+  int pre[MAXB + 1];  // the batch's paths, concatenated: iteration b owns queue slots [pre[b], pre[b+1])
+  pre[0] = 0;
+#pragma unroll
+  for (int b = 0; b < MAXB; b++) pre[b + 1] = pre[b] + (b < A.nb ? A.it[b].counts[A.depth] : 0);
+  const int n = pre[MAXB];
   if (MODE == TREE_LDS) {
     if (n == 0) return;  // uniform: nothing to trace
     const int words = 2 * S.num_nodes;
@@ -210,114 +259,102 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
   __syncthreads();
   int* work = A.work + A.depth;
   const unsigned long long rt0 = COUNT ? __builtin_amdgcn_s_memrealtime() : 0ull;
-  // First chunk: the wave's own index (no atomic -- thousands of waves start at once);
-  // later chunks from the shared counter, which starts past the statically taken ones.
+  const unsigned long long t_k0 = COUNT ? __builtin_readcyclecounter() : 0ull;
+  TraverseCounters cnt{};
+  WaveRay R;  // every field defined: idle lanes take part in the wave-level code with a finished ray
+  wave_ray_start(S, R, mk3(0.0f, 0.0f, 0.0f), mk3(0.0f, 0.0f, 1.0f), FLT_MAXV, -1, W);
+  R.done = true;
+  int pidx = -1;  // the lane's path (-1: idle)
+  int pb = 0;     // ... and the batch iteration it belongs to
+  // The first 64 paths of each wave are its own (no atomic: thousands of waves start at once); the
+  // counter hands out the rest, starting after them.
   const int nwaves = gridDim.x * (TRACE_BLOCK / 64);
-  int chunk = blockIdx.x * (TRACE_BLOCK / 64) + (threadIdx.x >> 6);
+  const int wid = blockIdx.x * (TRACE_BLOCK / 64) + (threadIdx.x >> 6);
+  bool first = true, exhausted = false;
+  const bool kd = S.has_obj && S.num_nodes > 0;
+  long long rounds = 0;
   while (true) {
-    if (__ballot(1) != ~0ull) {  // the chunk protocol needs the whole wave here
+    if (__ballot(1) != ~0ull) {  // the refill protocol needs the whole wave here
       atomicOr(S.fault, 4);
       break;
     }
-    // chunk -> [base, end) of trace-order slots
-    int base = chunk * A.cw[2], end = min(n, base + A.cw[2]);
-    if (A.koff) {
-      int c = chunk, cls = 0;
-      base = n;
-      end = n;
-      for (; cls < A.nclass; cls++) {
-        const int s0 = A.koff[cls * A.keys_per_class * A.ntiles_alloc];
-        const int s1 = cls + 1 < A.nclass ? A.koff[(cls + 1) * A.keys_per_class * A.ntiles_alloc] : n;
-        const int nc = (s1 - s0 + A.cw[cls] - 1) / A.cw[cls];
-        if (c < nc) {
-          base = s0 + c * A.cw[cls];
-          end = min(s1, base + A.cw[cls]);
-          break;
+    // ---- refill idle lanes ----
+    if (!exhausted) {
+      if (COUNT) prof_lap(W, -1);
+      const unsigned long long im = __ballot(pidx < 0);
+      if (im) {
+        int base;
+        bool last;
+        if (first) {  // static round: slots [wid*64, wid*64 + 64)
+          base = wid * 64;
+          first = false;
+          last = nwaves * 64 >= n;
+        } else {
+          int b = 0;
+          if (lane == 0) b = nwaves * 64 + atomicAdd(work, __popcll(im));
+          base = __shfl(b, 0);
+          last = base + __popcll(im) >= n;  // the counter only grows: later rounds find nothing
         }
-        c -= nc;
+        if (pidx < 0) {
+          const int k = base + (int)lane_prefix(im);
+          if (k < n) {
+            const int b = (k >= pre[1]) + (k >= pre[2]) + (k >= pre[3]);
+            const TraceIter& I = b == 0 ? A.it[0] : (b == 1 ? A.it[1] : (b == 2 ? A.it[2] : A.it[3]));
+            const int local = k - (b == 0 ? 0 : (b == 1 ? pre[1] : (b == 2 ? pre[2] : pre[3])));
+            const int i = I.perm ? I.perm[local] : local;
+            const float4 q0 = I.paths.p0[i], q1 = I.paths.p1[i];
+            if (fbits(I.paths.p2[i].w) > 0) {  // no work for finished paths (compaction off)
+              const int2 gh = I.geomhit[i];
+              pidx = i;
+              pb = b;
+              wave_ray_start(S, R, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z), u2f((uint32_t)gh.x), gh.y, W);
+              if (!kd) R.done = true;
+            }
+          }
+        }
+        exhausted = last;
       }
+      if (COUNT) prof_lap(W, PROF_SETUP_CYC);
     }
-    if (base >= n) {  // uniform
-      if (COUNT && lane == 0) {
-        const unsigned long long us10 = (__builtin_amdgcn_s_memrealtime() - rt0) / 1000;  // 100 MHz ticks
-        atomicAdd(&A.counters->life[us10 < 63 ? us10 : 63], 1ull);
-      }
-      if (lane == 0 && atomicAdd(&s_waves_done, 1) == TRACE_BLOCK / 64 - 1)
-        atomicMax(&A.trace_t[2 * A.depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+    const bool busy = pidx >= 0 && !R.done;
+    if (__any(busy)) {
+      const bool fastAABB = __all(!busy || (fabsf(R.invdir.x) < FLT_INFV && fabsf(R.invdir.y) < FLT_INFV &&
+                                            fabsf(R.invdir.z) < FLT_INFV));
+      if (MODE == TREE_LDS)
+        trace_phase<HYBRID, COUNT>(S, NodesPacked{s_tree},
+                                   ClustersInterleaved{reinterpret_cast<const float4*>(s_tree + 2 * S.num_nodes)}, R,
+                                   fastAABB, S.num_materials, cnt, W);
+      else if (MODE == TREE_PACKED)
+        trace_phase<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
+                                   S.num_materials, cnt, W);
+      else
+        trace_phase<HYBRID, COUNT>(S, NodesWide{S.nodes}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
+                                   S.num_materials, cnt, W);
+    }
+    // ---- finished rays: their hit record (what ShadeableIntersection would carry) ----
+    if (pidx >= 0 && R.done) {
+      const Hit& h = R.h;
+      const int code = h.hit_geom_index == -1 ? -1 : (h.obj_intersect ? -(R.objTri + 2) : h.hit_geom_index);
+      int2* hits = pb == 0 ? A.it[0].hits : (pb == 1 ? A.it[1].hits : (pb == 2 ? A.it[2].hits : A.it[3].hits));
+      hits[pidx] = make_int2(code, h.objMaterialIdx);
+      pidx = -1;
+    }
+    if (exhausted && !__any(pidx >= 0)) break;
+    if (++rounds > (1ll << 20)) {  // unreachable: every round finishes or advances some ray
+      if (lane == 0) atomicOr(S.fault, 8);
       break;
     }
-    const unsigned long long t_k0 = COUNT ? __builtin_readcyclecounter() : 0ull;
-    if (COUNT) prof_lap(W, -1);
-    const int slot = base + lane;
-    const bool valid = slot < end;
-    const int i = (A.perm && valid) ? A.perm[slot] : slot;
-    float4 q0 = make_float4(0, 0, 0, 0), q1 = make_float4(0, 0, 1, 0);
-    int bounces = 0;
-    if (valid) {
-      q0 = A.paths.p0[i];
-      q1 = A.paths.p1[i];
-      bounces = fbits(A.paths.p2[i].w);
-    }
-    Ray ray;
-    ray.origin = mk3(q0.x, q0.y, q0.z);
-    ray.direction = mk3(q1.x, q1.y, q1.z);
-    ray.isinside = false;
-    ray.sdepth = q0.w;
-    const bool active = valid && bounces > 0;
-    Hit h;
-    h.t_min = FLT_MAXV;
-    h.hit_geom_index = -1;
-    h.obj_intersect = false;
-    h.objMaterialIdx = -1;
-    h.ip = mk3(0, 0, 0);
-    h.normal = mk3(0, 0, 0);
-    if (COUNT) prof_lap(W, PROF_SETUP_CYC);
-    if (active) {
-      f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
-      float t = 0;
-      const f3 inv = mk3(1.0f / ray.direction.x, 1.0f / ray.direction.y, 1.0f / ray.direction.z);
-      const bool finite = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
-      for (int g = 0; g < S.num_geoms; g++) {
-        const DevGeom& G = S.geoms[g];
-        if (finite && !geom_may_hit(G, ray.origin, inv)) {
-          t = -1.0f;  // the exact test would miss
-        } else if (G.type == 1) {
-          t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
-        } else if (G.type == 0) {
-          t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
-        }
-        if (t > 0.0f && h.t_min > t) {
-          h.t_min = t;
-          h.hit_geom_index = g;
-        }
-      }
-    }
-    if (COUNT) prof_lap(W, PROF_GEOM_CYC);
-    TraverseCounters cnt{};
-    int objTri = -1;
-    if (S.has_obj && S.num_nodes > 0) {  // uniform: every lane of the wave takes part
-      if (MODE == TREE_LDS)
-        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesPacked{s_tree}, ClustersInterleaved{reinterpret_cast<const float4*>(s_tree + 2 * S.num_nodes)},
-                                                ray, active, h, S.num_materials, cnt, W);
-      else if (MODE == TREE_PACKED)
-        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ClustersSplit{S.cl_lo, S.cl_hi}, ray, active, h,
-                                                S.num_materials, cnt, W);
-      else
-        objTri = traverseKD_wave<HYBRID, COUNT>(S, NodesWide{S.nodes}, ClustersSplit{S.cl_lo, S.cl_hi}, ray, active, h,
-                                                S.num_materials, cnt, W);
-    }
-    if (valid && active) {
-      const int code = h.hit_geom_index == -1 ? -1 : (h.obj_intersect ? -(objTri + 2) : h.hit_geom_index);
-      A.hits[i] = make_int2(code, h.objMaterialIdx);
-    }
-    if (COUNT) {
-      prof_lap(W, PROF_POST_CYC);
-      flush_counters(A.counters, cnt, W, t_k0);
-    }
-    int next = 0;
-    if (lane == 0) next = nwaves + atomicAdd(work, 1);
-    chunk = __shfl(next, 0);
   }
+  if (COUNT) {
+    prof_lap(W, PROF_POST_CYC);
+    flush_counters(A.counters, cnt, W, t_k0);
+    if (lane == 0) {
+      const unsigned long long us10 = (__builtin_amdgcn_s_memrealtime() - rt0) / 1000;  // 100 MHz ticks
+      atomicAdd(&A.counters->life[us10 < 63 ? us10 : 63], 1ull);
+    }
+  }
+  if (lane == 0 && atomicAdd(&s_waves_done, 1) == TRACE_BLOCK / 64 - 1)
+    atomicMax(&A.trace_t[2 * A.depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // ---------------------------------------------------------------------------
@@ -353,7 +390,7 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   if (i == 0) {
     atomicAdd(A.total_segments, (unsigned long long)n);
     const unsigned long long t0 = A.trace_t[2 * A.depth], t1 = A.trace_t[2 * A.depth + 1];
-    if (t1 > t0) {  // the intersect launch before this one on the stream ran (n > 0)
+    if (A.trace_total && t1 > t0) {  // the intersect launch before this one on the stream ran (n > 0)
       atomicAdd(&A.trace_total[0], t1 - t0);
       atomicAdd(&A.trace_total[1], 1ull);
     }
@@ -641,6 +678,7 @@ struct kdpt_ctx {
   int* counts = nullptr;  // [cap + 2] live paths per bounce, [cap + 2] fault flag, then [cap] work counters
   int* work = nullptr;
   int2* hits = nullptr;   // [npix] hit code + objMaterialIdx from the intersect kernel
+  int2* geomhit = nullptr;  // [npix] analytic-geom t_min bits + index (k_geoms -> k_trace)
   int tree_mode = 0;      // TreeMode
   int trace_grid = 0;     // persistent intersect workgroups
   size_t tree_lds = 0;    // dynamic LDS bytes of the intersect kernel (TREE_LDS)
@@ -668,6 +706,7 @@ struct kdpt_ctx {
   // images are added into `image` in iteration order on `accum_stream`.
   kdpt_ctx* parent = nullptr;
   std::vector<kdpt_ctx*> slots;
+  int slot_batch = 1;
   std::vector<hipEvent_t> slot_done, slot_free;
   hipStream_t accum_stream = nullptr;
   // intersect-kernel timing (testing_mode) of every iteration, read back at synchronisation
@@ -698,6 +737,8 @@ int dupload(kdpt_ctx* c, T** p, const T* src, size_t n) {
 }
 
 int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count);
+int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, int stop_depth, bool count,
+                 std::vector<hipEvent_t>* bev);
 
 // stats.segments / seg_per_bounce / bounces of the iteration whose counts are in h_counts
 int segments_from_counts(kdpt_ctx* c) {
@@ -732,6 +773,7 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
   if ((rc = dalloc(c, &c->trace_t, 2 * (size_t)c->cap))) return rc;
   HIP_TRY(hipMemset(c->trace_t, 0, sizeof(unsigned long long) * 2 * c->cap));
   if ((rc = dalloc(c, &c->counts, 2 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
+      (rc = dalloc(c, &c->geomhit, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->perm, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->tile_kcounts, (size_t)TRACE_KEYS * c->ntiles)) ||
       (rc = dalloc(c, &c->tile_koff, (size_t)TRACE_KEYS * c->ntiles)) ||
@@ -1287,37 +1329,63 @@ int kdpt_trace_iteration(kdpt_ctx* c, int frame, int iter) {
   return KDPT_OK;
 }
 
-int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int stride, int pipeline) {
+int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int stride, int pipeline, int batch) {
   (void)frame;
   if (!c || count < 0 || first_iter < 1 || stride < 1) return fail(KDPT_ERR_ARG, "bad arguments");
   if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
   HIP_TRY(hipSetDevice(c->device));
   const int depth = std::min(8, std::max(1, pipeline));
+  const int B = std::min(MAXB, std::max(1, batch));
   if (!c->accum_stream) HIP_TRY(hipStreamCreateWithFlags(&c->accum_stream, hipStreamNonBlocking));
   // the accumulation follows everything already queued on the context's own stream (reset, ...)
   hipEvent_t entry;
   HIP_TRY(hipEventCreate(&entry));
   HIP_TRY(hipEventRecord(entry, c->stream));
   HIP_TRY(hipStreamWaitEvent(c->accum_stream, entry, 0));
-  while ((int)c->slots.size() < depth) {
-    kdpt_ctx* sl = nullptr;
-    int rc = make_slot(c, &sl);
-    if (rc) return rc;
-    c->slots.push_back(sl);
-    hipEvent_t d, f;
-    HIP_TRY(hipEventCreateWithFlags(&d, hipEventDisableTiming));
-    HIP_TRY(hipEventCreateWithFlags(&f, hipEventDisableTiming));
-    HIP_TRY(hipEventRecord(f, c->accum_stream));
-    c->slot_done.push_back(d);
-    c->slot_free.push_back(f);
+  // slots: `depth` groups of B iteration contexts; a group runs one batch at a time on its first
+  // context's stream
+  if ((int)c->slots.size() < depth * B || c->slot_batch != B) {
+    if (!c->slots.empty()) {
+      int rc = kdpt_synchronize(c);
+      if (rc) return rc;
+      for (auto sl : c->slots) kdpt_destroy(sl);
+      for (auto e : c->slot_done) (void)hipEventDestroy(e);
+      for (auto e : c->slot_free) (void)hipEventDestroy(e);
+      c->slots.clear();
+      c->slot_done.clear();
+      c->slot_free.clear();
+    }
+    c->slot_batch = B;
+    while ((int)c->slots.size() < depth * B) {
+      kdpt_ctx* sl = nullptr;
+      int rc = make_slot(c, &sl);
+      if (rc) return rc;
+      c->slots.push_back(sl);
+    }
+    for (int g = 0; g < depth; g++) {
+      hipEvent_t d, f;
+      HIP_TRY(hipEventCreateWithFlags(&d, hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&f, hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(f, c->accum_stream));
+      c->slot_done.push_back(d);
+      c->slot_free.push_back(f);
+    }
   }
-  for (int k = 0; k < count; k++) {
-    const int si = k % depth;
-    kdpt_ctx* sl = c->slots[si];
-    HIP_TRY(hipStreamWaitEvent(sl->stream, c->slot_free[si], 0));  // its last partial image was consumed
-    HIP_TRY(hipMemsetAsync(sl->image, 0, sizeof(float) * 3 * (size_t)c->npix, sl->stream));
-    std::vector<hipEvent_t> evs;
+  const int ngroups = (int)c->slot_done.size();
+  for (int kb = 0, bi = 0; kb < count; kb += B, bi++) {
+    const int nb = std::min(B, count - kb);
+    const int g = bi % ngroups;
+    kdpt_ctx* const* grp = &c->slots[(size_t)g * B];
+    hipStream_t st = grp[0]->stream;
+    HIP_TRY(hipStreamWaitEvent(st, c->slot_free[g], 0));  // the group's last partial images were consumed
+    int iters[MAXB];
+    for (int b = 0; b < nb; b++) {
+      iters[b] = first_iter + (kb + b) * stride;
+      HIP_TRY(hipMemsetAsync(grp[b]->image, 0, sizeof(float) * 3 * (size_t)c->npix, st));
+    }
+    std::vector<hipEvent_t>* bev = nullptr;
     if (c->opt.testing_mode) {
+      std::vector<hipEvent_t> evs;
       for (int e = 0; e < 2 * c->cap; e++) {
         hipEvent_t ev;
         if (!c->free_ev.empty()) { ev = c->free_ev.back(); c->free_ev.pop_back(); }
@@ -1325,17 +1393,19 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
         evs.push_back(ev);
       }
       c->pending_ev.push_back(evs);
-      sl->rec_ev = &c->pending_ev.back();
+      bev = &c->pending_ev.back();
     }
-    int rc = launch_iteration(sl, first_iter + k * stride, -1, false);
-    sl->rec_ev = nullptr;
+    int rc = launch_batch(grp, iters, nb, st, -1, false, bev);
     if (rc) return rc;
-    HIP_TRY(hipEventRecord(c->slot_done[si], sl->stream));
-    HIP_TRY(hipStreamWaitEvent(c->accum_stream, c->slot_done[si], 0));
+    HIP_TRY(hipEventRecord(c->slot_done[g], st));
+    HIP_TRY(hipStreamWaitEvent(c->accum_stream, c->slot_done[g], 0));
     const int n3 = 3 * c->npix;
-    hipLaunchKernelGGL(k_accumulate, dim3((n3 + 255) / 256), dim3(256), 0, c->accum_stream, c->image, sl->image, n3);
-    HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(c->slot_free[si], c->accum_stream));
+    for (int b = 0; b < nb; b++) {  // in iteration order
+      hipLaunchKernelGGL(k_accumulate, dim3((n3 + 255) / 256), dim3(256), 0, c->accum_stream, c->image,
+                         grp[b]->image, n3);
+      HIP_TRY(hipGetLastError());
+    }
+    HIP_TRY(hipEventRecord(c->slot_free[g], c->accum_stream));
   }
   HIP_TRY(hipEventDestroy(entry));
   c->stats.iterations += count;
@@ -1533,127 +1603,149 @@ int kdpt_selftest_fresnel(const float* cs, int n, float ior, float* f) {
 namespace {
 
 template <bool HYBRID, bool COUNT>
-void launch_trace_mode(kdpt_ctx* c, const TraceArgs& a) {
+void launch_trace_mode(kdpt_ctx* c, const TraceArgs& a, hipStream_t st) {
   const dim3 g(c->trace_grid), b(TRACE_BLOCK);
   if (c->tree_mode == TREE_LDS)
-    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS>), g, b, c->tree_lds, c->stream, a);
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS>), g, b, c->tree_lds, st, a);
   else if (c->tree_mode == TREE_PACKED)
-    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_PACKED>), g, b, 0, c->stream, a);
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_PACKED>), g, b, 0, st, a);
   else
-    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_WIDE>), g, b, 0, c->stream, a);
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_WIDE>), g, b, 0, st, a);
 }
 
-void launch_trace(kdpt_ctx* c, const TraceArgs& a, bool count) {
+void launch_trace(kdpt_ctx* c, const TraceArgs& a, bool count, hipStream_t st) {
   const bool hyb = c->opt.short_stack != 0;
-  if (hyb) { if (count) launch_trace_mode<true, true>(c, a); else launch_trace_mode<true, false>(c, a); }
-  else { if (count) launch_trace_mode<false, true>(c, a); else launch_trace_mode<false, false>(c, a); }
+  if (hyb) { if (count) launch_trace_mode<true, true>(c, a, st); else launch_trace_mode<true, false>(c, a, st); }
+  else { if (count) launch_trace_mode<false, true>(c, a, st); else launch_trace_mode<false, false>(c, a, st); }
 }
 
 template <bool HYBRID>
-void launch_shade_h(kdpt_ctx* c, const ShadeArgs& a, bool compact, bool sort) {
+void launch_shade_h(kdpt_ctx* c, const ShadeArgs& a, bool compact, bool sort, hipStream_t st) {
   const dim3 g(c->ntiles), b(TILE);
   if (compact) {
-    if (sort) hipLaunchKernelGGL((k_shade<HYBRID, true, true>), g, b, 0, c->stream, a);
-    else hipLaunchKernelGGL((k_shade<HYBRID, true, false>), g, b, 0, c->stream, a);
+    if (sort) hipLaunchKernelGGL((k_shade<HYBRID, true, true>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((k_shade<HYBRID, true, false>), g, b, 0, st, a);
   } else {
-    if (sort) hipLaunchKernelGGL((k_shade<HYBRID, false, true>), g, b, 0, c->stream, a);
-    else hipLaunchKernelGGL((k_shade<HYBRID, false, false>), g, b, 0, c->stream, a);
+    if (sort) hipLaunchKernelGGL((k_shade<HYBRID, false, true>), g, b, 0, st, a);
+    else hipLaunchKernelGGL((k_shade<HYBRID, false, false>), g, b, 0, st, a);
   }
 }
 
-int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
-  const int gen_iter = c->opt.cacherays ? 1 : iter;
-  c->cur = 0;
-  hipLaunchKernelGGL(k_gen_rays, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->cam, gen_iter,
-                     c->traceDepth, c->buf[0], c->opt.focal_length, c->opt.dof_angle, c->opt.antialias, c->counts,
-                     c->cap + 2, c->work, c->cap, c->trace_t);
-  HIP_TRY(hipGetLastError());
-  const bool compact = c->opt.compaction != 0;
-  const bool sort = (iter == 2);
-  for (int depth = 0; depth < c->cap; depth++) {
-    TraceArgs t;
-    t.S = c->S;
-    t.paths = c->buf[c->cur];
-    t.perm = (depth > 0 && compact && c->trace_order) ? c->perm : nullptr;
-    t.koff = t.perm ? c->tile_koff : nullptr;
-    t.ntiles_alloc = c->ntiles;
-    t.keys_per_class = c->S.trace_mode == 1 ? 8 : 1;
-    t.nclass = c->S.trace_mode == 2 ? 1 : 3;
-    for (int k = 0; k < 3; k++) t.cw[k] = c->chunk_width[k];
-    t.hits = c->hits;
-    t.counts = c->counts;
-    t.work = c->work;
-    t.depth = depth;
-    t.counters = c->counters;
-    t.trace_t = c->trace_t;
-    std::vector<hipEvent_t>& bev = c->rec_ev ? *c->rec_ev : c->bounce_ev;
-    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(bev[2 * depth], c->stream));
-    launch_trace(c, t, count);
+// One iteration of each context in cs (nb <= MAXB; all share the scene and options), in lockstep on
+// stream st: per bounce the analytic geoms of each, one intersect launch over all of them, then each
+// one's shading and compaction.  The iterations stay independent: only the intersect launch is shared.
+int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, int stop_depth, bool count,
+                 std::vector<hipEvent_t>* bev) {
+  kdpt_ctx* c0 = cs[0];
+  for (int b = 0; b < nb; b++) {
+    kdpt_ctx* c = cs[b];
+    const int gen_iter = c->opt.cacherays ? 1 : iters[b];
+    c->cur = 0;
+    hipLaunchKernelGGL(k_gen_rays, dim3((c->npix + 255) / 256), dim3(256), 0, st, c->cam, gen_iter, c->traceDepth,
+                       c->buf[0], c->opt.focal_length, c->opt.dof_angle, c->opt.antialias, c->counts, c->cap + 2,
+                       c->work, c->cap, c->trace_t);
     HIP_TRY(hipGetLastError());
-    if (c->sync_debug) {
-      fprintf(stderr, "[kdpt] trace depth %d launched (grid %d, mode %d, lds %zu)\n", depth, c->trace_grid,
-              c->tree_mode, c->tree_lds);
-      HIP_TRY(hipStreamSynchronize(c->stream));
+  }
+  const bool compact = c0->opt.compaction != 0;
+  for (int depth = 0; depth < c0->cap; depth++) {
+    if (c0->opt.testing_mode && bev) HIP_TRY(hipEventRecord((*bev)[2 * depth], st));
+    TraceArgs t;
+    t.S = c0->S;
+    t.nb = nb;
+    for (int b = 0; b < MAXB; b++) {
+      kdpt_ctx* c = cs[b < nb ? b : 0];
+      t.it[b].paths = c->buf[c->cur];
+      t.it[b].perm = (depth > 0 && compact && c->trace_order) ? c->perm : nullptr;
+      t.it[b].geomhit = c->geomhit;
+      t.it[b].hits = c->hits;
+      t.it[b].counts = c->counts;
+    }
+    t.work = c0->work;
+    t.depth = depth;
+    t.counters = c0->counters;
+    t.trace_t = c0->trace_t;
+    for (int b = 0; b < nb; b++) {
+      kdpt_ctx* c = cs[b];
+      hipLaunchKernelGGL(k_geoms, dim3(c->ntiles), dim3(TILE), 0, st, c->S, c->buf[c->cur], c->counts, depth,
+                         c->geomhit);
+      HIP_TRY(hipGetLastError());
+    }
+    launch_trace(c0, t, count, st);
+    HIP_TRY(hipGetLastError());
+    if (c0->sync_debug) {
+      fprintf(stderr, "[kdpt] trace depth %d launched (grid %d, mode %d, lds %zu, batch %d)\n", depth,
+              c0->trace_grid, c0->tree_mode, c0->tree_lds, nb);
+      HIP_TRY(hipStreamSynchronize(st));
       fprintf(stderr, "[kdpt] trace depth %d done\n", depth);
     }
-    if (c->opt.testing_mode) HIP_TRY(hipEventRecord(bev[2 * depth + 1], c->stream));
-    ShadeArgs a;
-    a.S = c->S;
-    a.paths = c->buf[c->cur];
-    a.hits = c->hits;
-    a.image = c->image;
-    a.counts = c->counts;
-    a.depth = depth;
-    a.iter = iter;
-    a.softness = c->opt.softness;
-    a.enable_sss = c->opt.enable_sss;
-    a.tile_counts = c->tile_counts;
-    a.tile_kcounts = (compact && c->trace_order) ? c->tile_kcounts : nullptr;
-    a.ntiles = c->ntiles;
-    a.nkeys = c->nkeys;
-    a.total_segments = c->total_segments;
-    a.trace_t = c->trace_t;
-    a.trace_total = c->trace_total;
-    if (c->opt.short_stack) launch_shade_h<true>(c, a, compact, sort);
-    else launch_shade_h<false>(c, a, compact, sort);
-    HIP_TRY(hipGetLastError());
-    if (c->sync_debug) {
-      HIP_TRY(hipStreamSynchronize(c->stream));
-      fprintf(stderr, "[kdpt] shade depth %d done\n", depth);
-    }
-    if (compact || sort) {
-      hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, c->stream, c->tile_counts, c->tile_off, c->counts, depth,
-                         c->ntiles, sort ? c->nkeys : 1, 1);
+    if (c0->opt.testing_mode && bev) HIP_TRY(hipEventRecord((*bev)[2 * depth + 1], st));
+    for (int b = 0; b < nb; b++) {
+      kdpt_ctx* c = cs[b];
+      const bool sort = (iters[b] == 2);
+      ShadeArgs a;
+      a.S = c->S;
+      a.paths = c->buf[c->cur];
+      a.hits = c->hits;
+      a.image = c->image;
+      a.counts = c->counts;
+      a.depth = depth;
+      a.iter = iters[b];
+      a.softness = c->opt.softness;
+      a.enable_sss = c->opt.enable_sss;
+      a.tile_counts = c->tile_counts;
+      a.tile_kcounts = (compact && c->trace_order) ? c->tile_kcounts : nullptr;
+      a.ntiles = c->ntiles;
+      a.nkeys = c->nkeys;
+      a.total_segments = c->total_segments;
+      a.trace_t = c0->trace_t;
+      a.trace_total = b == 0 ? c->trace_total : nullptr;
+      if (c->opt.short_stack) launch_shade_h<true>(c, a, compact, sort, st);
+      else launch_shade_h<false>(c, a, compact, sort, st);
       HIP_TRY(hipGetLastError());
-      const bool order = compact && c->trace_order;
-      if (order) {
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, c->stream, c->tile_kcounts, c->tile_koff, c->counts,
-                           depth, c->ntiles, TRACE_KEYS, 0);
+      if (compact || sort) {
+        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, c->tile_counts, c->tile_off, c->counts, depth,
+                           c->ntiles, sort ? c->nkeys : 1, 1);
         HIP_TRY(hipGetLastError());
+        const bool order = compact && c->trace_order;
+        if (order) {
+          hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, c->tile_kcounts, c->tile_koff, c->counts, depth,
+                             c->ntiles, TRACE_KEYS, 0);
+          HIP_TRY(hipGetLastError());
+        }
+        const int nxt = c->cur ^ 1;
+        int* perm = order ? c->perm : nullptr;
+        if (sort)
+          hipLaunchKernelGGL(k_scatter<true>, dim3(c->ntiles), dim3(TILE), 0, st, c->buf[c->cur], c->buf[nxt],
+                             c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, c->tile_koff, perm, c->S);
+        else
+          hipLaunchKernelGGL(k_scatter<false>, dim3(c->ntiles), dim3(TILE), 0, st, c->buf[c->cur], c->buf[nxt],
+                             c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, c->tile_koff, perm, c->S);
+        HIP_TRY(hipGetLastError());
+        c->cur = nxt;
+      } else {
+        // no compaction, no sort: the live range stays the whole image
+        HIP_TRY(hipMemcpyAsync(c->counts + depth + 1, c->counts + depth, sizeof(int), hipMemcpyDeviceToDevice, st));
       }
-      const int nxt = c->cur ^ 1;
-      int* perm = order ? c->perm : nullptr;
-      if (sort)
-        hipLaunchKernelGGL(k_scatter<true>, dim3(c->ntiles), dim3(TILE), 0, c->stream, c->buf[c->cur], c->buf[nxt],
-                           c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, c->tile_koff, perm, c->S);
-      else
-        hipLaunchKernelGGL(k_scatter<false>, dim3(c->ntiles), dim3(TILE), 0, c->stream, c->buf[c->cur], c->buf[nxt],
-                           c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, c->tile_koff, perm, c->S);
-      HIP_TRY(hipGetLastError());
-      c->cur = nxt;
-    } else {
-      // no compaction, no sort: the live range stays the whole image
-      HIP_TRY(hipMemcpyAsync(c->counts + depth + 1, c->counts + depth, sizeof(int), hipMemcpyDeviceToDevice,
-                             c->stream));
+    }
+    if (c0->sync_debug) {
+      HIP_TRY(hipStreamSynchronize(st));
+      fprintf(stderr, "[kdpt] shade depth %d done\n", depth);
     }
     if (stop_depth == depth) return KDPT_OK;
   }
   if (!compact) {
-    hipLaunchKernelGGL(k_final_gather, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->buf[c->cur],
-                       c->counts, c->cap, c->image);
-    HIP_TRY(hipGetLastError());
+    for (int b = 0; b < nb; b++) {
+      kdpt_ctx* c = cs[b];
+      hipLaunchKernelGGL(k_final_gather, dim3((c->npix + 255) / 256), dim3(256), 0, st, c->buf[c->cur], c->counts,
+                         c->cap, c->image);
+      HIP_TRY(hipGetLastError());
+    }
   }
   return KDPT_OK;
+}
+
+int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
+  return launch_batch(&c, &iter, 1, c->stream, stop_depth, count, c->rec_ev ? c->rec_ev : &c->bounce_ev);
 }
 
 }  // namespace

@@ -130,7 +130,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_create.argtypes = [P(Scene), P(Options), C.c_int, P(C.c_void_p)]
     lib.kdpt_trace_iteration.argtypes = [C.c_void_p, C.c_int, C.c_int]
     lib.kdpt_trace_iteration_async.argtypes = [C.c_void_p, C.c_int, C.c_int]
-    lib.kdpt_trace_iterations.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
+    lib.kdpt_trace_iterations.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int]
     lib.kdpt_synchronize.argtypes = [C.c_void_p]
     lib.kdpt_read_image.argtypes = [C.c_void_p, P(C.c_float)]
     lib.kdpt_write_pbo.argtypes = [C.c_void_p, C.c_int, P(C.c_uint8)]
@@ -320,10 +320,12 @@ class PathTracer:
     def trace_iteration_async(self, iteration: int, frame: int = 0):
         _check(self.lib.kdpt_trace_iteration_async(self._ctx, int(frame), int(iteration)), "kdpt_trace_iteration_async")
 
-    def trace_iterations(self, first: int, count: int, stride: int = 1, pipeline: int = 3, frame: int = 0):
-        """Iterations first + k*stride (k < count), `pipeline` in flight (kdpt_trace_iterations; async)."""
+    def trace_iterations(self, first: int, count: int, stride: int = 1, pipeline: int = 3, batch: int = 1,
+                         frame: int = 0):
+        """Iterations first + k*stride (k < count): batches of `batch` sharing each intersect launch,
+        `pipeline` batches in flight (kdpt_trace_iterations; async)."""
         _check(self.lib.kdpt_trace_iterations(self._ctx, int(frame), int(first), int(count), int(stride),
-                                              int(pipeline)), "kdpt_trace_iterations")
+                                              int(pipeline), int(batch)), "kdpt_trace_iterations")
 
     def synchronize(self):
         _check(self.lib.kdpt_synchronize(self._ctx), "kdpt_synchronize")

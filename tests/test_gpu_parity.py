@@ -186,10 +186,11 @@ def test_soft_branch_within_tolerance(kdpt, oracle, opts):
     assert same > 0.99, same
 
 
-@pytest.mark.parametrize("pipeline", [1, 3])
-def test_pipelined_iterations_bit_exact(kdpt, pipeline):
-    """kdpt_trace_iterations (several iterations in flight, partial images added in order) gives the
-    same image bits and segment counts as one kdpt_trace_iteration after another."""
+@pytest.mark.parametrize("pipeline,batch", [(1, 1), (3, 1), (2, 3), (1, 4)])
+def test_pipelined_iterations_bit_exact(kdpt, pipeline, batch):
+    """kdpt_trace_iterations (batches sharing intersect launches, several batches in flight, partial
+    images added in order) gives the same image bits and segment counts as one kdpt_trace_iteration
+    after another."""
     desc = load_fixture_scene("cornell", "dragon_5", res=(96, 80), depth=8)
     sd = kdpt.SceneData.from_description(desc)
     seq = kdpt.PathTracer(sd, kdpt.default_options())
@@ -199,7 +200,7 @@ def test_pipelined_iterations_bit_exact(kdpt, pipeline):
     tot_seq = seq.stats().total_segments
     seq.close()
     pip = kdpt.PathTracer(sd, kdpt.default_options())
-    pip.trace_iterations(1, 7, pipeline=pipeline)
+    pip.trace_iterations(1, 7, pipeline=pipeline, batch=batch)
     pip.synchronize()
     img_pip = pip.image()
     tot_pip = pip.stats().total_segments
