@@ -649,7 +649,10 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     // Few lanes still walking and many waiting on leaves: test those leaves now; the walkers keep
     // their state and resume in the next node phase (their own sequence of steps is unchanged).
     if (__popcll(wmask) <= S.early_walk && __popcll(__ballot((fl & F_LEAF) != 0u)) >= S.early_leaf) break;
-    if (COUNT) trips += walk ? 1 : 0;
+    if (COUNT) {
+      trips += walk ? 1 : 0;
+      prof_add(W, PROF_SPARE, (unsigned long long)__popcll(wmask));  // lane-steps: SIMD efficiency
+    }
     const NodeRec nd = nodes(cur < 0 ? 0 : cur);
     const int left = nd.left, right = nd.right;
     const uint32_t Lu = (uint32_t)L;

@@ -707,6 +707,7 @@ struct kdpt_ctx {
   kdpt_ctx* parent = nullptr;
   std::vector<kdpt_ctx*> slots;
   int slot_batch = 1;
+  bool profile_batches = false;
   std::vector<hipEvent_t> slot_done, slot_free;
   hipStream_t accum_stream = nullptr;
   // intersect-kernel timing (testing_mode) of every iteration, read back at synchronisation
@@ -1297,6 +1298,7 @@ int kdpt_synchronize(kdpt_ctx* c) {
   if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
   int rc = drain_intersect_events(c);
   if (rc) return rc;
+  if (c->profile_batches) HIP_TRY(hipMemcpy(&c->last_profile, c->counters, sizeof(Counters), hipMemcpyDeviceToHost));
   return check_fault(c);
 }
 
@@ -1372,6 +1374,11 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
     }
   }
   const int ngroups = (int)c->slot_done.size();
+  {  // diagnostic: KDPT_PROFILE_BATCHES=1 runs the counting intersect kernel (kdpt_wave_profile after sync)
+    const char* e = getenv("KDPT_PROFILE_BATCHES");
+    c->profile_batches = e && e[0] == '1';
+    if (c->profile_batches) HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(Counters), c->stream));
+  }
   for (int kb = 0, bi = 0; kb < count; kb += B, bi++) {
     const int nb = std::min(B, count - kb);
     const int g = bi % ngroups;
@@ -1395,7 +1402,7 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
       c->pending_ev.push_back(evs);
       bev = &c->pending_ev.back();
     }
-    int rc = launch_batch(grp, iters, nb, st, -1, false, bev);
+    int rc = launch_batch(grp, iters, nb, st, -1, c->profile_batches, bev);
     if (rc) return rc;
     HIP_TRY(hipEventRecord(c->slot_done[g], st));
     HIP_TRY(hipStreamWaitEvent(c->accum_stream, c->slot_done[g], 0));

@@ -373,7 +373,7 @@ class PathTracer:
         n = self.lib.kdpt_wave_profile(self._ctx, out, 128)
         _check(0 if n > 0 else n, "kdpt_wave_profile")
         keys = ("node_trips", "node_cycles", "big_sweeps", "big_cycles", "small_phases", "small_rounds",
-                "small_cycles", "final_cycles", "setup_cycles", "geom_cycles", "post_cycles", "spare",
+                "small_cycles", "final_cycles", "setup_cycles", "geom_cycles", "post_cycles", "node_lane_steps",
                 "chunks", "chunk_cycles", "aabb", "tri", "hit")
         prof = dict(zip(keys, (int(out[k]) for k in range(len(keys)))))
         if n > len(keys):

@@ -1,0 +1,28 @@
+"""Wave profile of the intersect kernel under kdpt_trace_iterations (KDPT_PROFILE_BATCHES=1)."""
+import json
+import os
+import sys
+
+os.environ["KDPT_PROFILE_BATCHES"] = "1"
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
+    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: F401
+from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options, load_fixture_scene
+
+sd = SceneData.from_description(load_fixture_scene("cornell", sys.argv[1] if len(sys.argv) > 1 else "dragon_5",
+                                                   res=(800, 800), depth=8))
+for cfg in (sys.argv[2] if len(sys.argv) > 2 else "1x1,2x2,1x4").split(","):
+    p, b = (int(v) for v in cfg.split("x"))
+    pt = PathTracer(sd, default_options(testing_mode=1))
+    pt.trace_iterations(1, 8, pipeline=p, batch=b)
+    pt.synchronize()
+    prof = pt.wave_profile()
+    prof.pop("wave_life_10us", None)
+    w = max(1, prof["chunks"])
+    eff = prof["node_lane_steps"] / max(1, prof["node_trips"]) / 64
+    print(json.dumps({"cfg": cfg, "waves": w, "node_trips_per_wave": round(prof["node_trips"] / w, 1),
+                      "node_simd_eff": round(eff, 3), "small_phases_per_wave": round(prof["small_phases"] / w, 1),
+                      "cyc_frac": {k: round(prof[k] / max(1, prof["chunk_cycles"]), 3)
+                                   for k in prof if k.endswith("_cycles") and k != "chunk_cycles"}}), flush=True)
+    pt.close()
