@@ -127,6 +127,18 @@ typedef struct kdpt_scene {
     int num_tris;
     const int *obj_materialOffsets; /* one per OBJ shape */
     int num_shapes;
+    /* enable_kd = 0 only (brute force, pathTraceOneBounce src/pathtrace.cu:402-628): the raw OBJ arrays
+       pathtraceInit uploads in that mode (src/pathtrace.cu:225-257), as Scene::loadObj builds them
+       (src/scene.cpp:603-712).  Ignored when enable_kd = 1. */
+    const float *obj_verts;      /* attrib.vertices: 3 floats per vertex index */
+    int num_obj_verts;           /* floats */
+    const float *obj_norms;      /* attrib.normals, read at 3*vertex_index like the reference */
+    int num_obj_norms;           /* floats */
+    const int *obj_polyoffsets;  /* per shape: number of vertex indices (3 per triangle) */
+    const int *obj_polysidxflat; /* vertex indices, shape after shape */
+    int polyidxcount;
+    const float *obj_bboxes;     /* Scene::obj_bboxes; shape i's box is read at [i .. i+5] (use_bbox) */
+    int num_bbox_floats;
 } kdpt_scene;
 
 /* The flags of pathtrace() with src/main.cpp:35-60 defaults (kdpt_default_options). */
@@ -139,9 +151,9 @@ typedef struct kdpt_options {
     int enable_sss;      /* 0 */
     int testing_mode;    /* 0: 1 = also time the intersect kernel per bounce (TESTINGMODE) */
     int compaction;      /* 1 */
-    int enable_kd;       /* 1 (0 = brute force, not built: KDPT_ERR_UNSUPPORTED) */
+    int enable_kd;       /* 1; 0 = brute force over the OBJ arrays (pathTraceOneBounce) */
     int viz_kd;          /* 0 (box visualisation, not built) */
-    int use_bbox;        /* 0 */
+    int use_bbox;        /* 0; brute force only: each shape's bbox test first (src/pathtrace.cu:497-513) */
     int short_stack;     /* 1: traverseKDbareShortHybrid, 0: traverseKDbare */
     int bounce_cap;      /* 8 == `depth > 7` (src/pathtrace.cu:2608); 16 for the stress config */
     int block_size;      /* 0 = default (256) */

@@ -358,6 +358,182 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// pathTraceOneBounce (src/pathtrace.cu:402-628, enable_kd = false): the brute-force intersect kernel,
+// the reference's "bruteforce" / "bbox" benchmark columns.  One lane per live path, consecutive paths
+// per wave; the analytic geoms, then every OBJ triangle in file order, shape after shape.
+//
+// The triangle index is wave-uniform (every lane of a wave tests the same triangle), so the triangle
+// is fetched with scalar loads once per wave.  Each lane first evaluates, without the division,
+// the exact values the reference's Moller-Trumbore divides (a, u = dot(s,p), v = dot(d,q),
+// w = dot(e2,q): same operations, same order, so the same bits) and rejects the triangle when the
+// decision is certain whatever f = 1/a rounds to; only the remaining lanes (the line crosses the
+// triangle, or a decision sits within a few ulps of its threshold) run the reference's exact test and
+// hit point.  Output: the same hit record as k_trace (code, objMaterialIdx).
+// ---------------------------------------------------------------------------
+struct BruteShape {
+  float4 lo;  // bbox min (the reference's float(obj_polysbboxes[i + k] - 0.01)), w = index count bits
+  float4 hi;  // bbox max (+ 0.01), w = obj_materialOffsets[i] bits
+};
+
+struct BruteArgs {
+  DevScene S;  // tv0/te1/te2/tn0..2: the OBJ triangles in file order
+  PathBuf paths;
+  const int* counts;
+  int depth;
+  int2* hits;
+  const BruteShape* shapes;
+  int num_shapes;
+  Counters* counters;
+  unsigned long long* trace_t;
+};
+
+// intersectBbox (src/interactions.h:136-165), std::min/max as in intersectAABBarrays
+__device__ inline float intersectBbox(f3 o, f3 d, float4 lo, float4 hi) {
+  const f3 invdir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const float v1 = (lo.x - o.x) * invdir.x, v2 = (hi.x - o.x) * invdir.x;
+  const float v3 = (lo.y - o.y) * invdir.y, v4 = (hi.y - o.y) * invdir.y;
+  const float v5 = (lo.z - o.z) * invdir.z, v6 = (hi.z - o.z) * invdir.z;
+  const float dmin = std_max(std_max(std_min(v1, v2), std_min(v3, v4)), std_min(v5, v6));
+  const float dmax = std_min(std_min(std_max(v1, v2), std_max(v3, v4)), std_max(v5, v6));
+  if (dmax < 0) return dmax;
+  if (dmin > dmax) return dmax;
+  return dmin;
+}
+
+// Is glm::intersectRayTriangle certain to return false?  a, u, v, w are the reference's exact values;
+// f = RN(1/a) > 0 (a >= eps).  bx = RN(f*u) < 0 for u < -a*2^-100 (|f*u| >= 2^-101, far from rounding
+// to -0); bx > 1 for u > RN(a*(1+2^-20)) (then u/a > 1 + 2^-21 and two roundings cannot bring it to 1);
+// likewise by, the sum (u + v > a*(1+2^-18) with u, v >= 0) and bz = RN(f*w) < 0.
+__device__ inline bool tri_certain_miss(float a, float u, float v, float w) {
+  const float tiny = a * 0x1p-100f;
+  const float one_u = a * 1.00000095367431640625f;  // a * (1 + 2^-20)
+  const float one_s = a * 1.000003814697265625f;    // a * (1 + 2^-18)
+  return !(a >= FLT_EPS) || u < -tiny || u > one_u || v < -tiny || w < -tiny ||
+         (u >= 0.0f && v >= 0.0f && u + v > one_s);
+}
+
+template <bool COUNT>
+__device__ inline void brute_triangle(const DevScene& S, int k, const TriData& T, f3 o, f3 d, float& t_min, int& best,
+                                      bool take, TraverseCounters& cnt) {
+  const f3 v0 = mk3(T.v0.x, T.v0.y, T.v0.z), e1 = mk3(T.e1.x, T.e1.y, T.e1.z), e2 = mk3(T.e2.x, T.e2.y, T.e2.z);
+  const f3 p = cross(d, e2);
+  const float a = dot(e1, p);
+  const f3 s = sub(o, v0);
+  const float u = dot(s, p);
+  const f3 q = cross(s, e1);
+  const float v = dot(d, q);
+  const float w = dot(e2, q);
+  if (take && !tri_certain_miss(a, u, v, w)) {
+    float bx, by, bz;
+    if (tri_test_v(T, o, d, bx, by, bz) == 2) {  // intersected: bary.z >= 0
+      if (COUNT) cnt.hit++;
+      f3 hp, nn;
+      const float t = tri_hit_t<true>(S, k, o, d, bx, by, bz, hp, nn);  // hit += norm * 0.0001f
+      if (t > 0.0f && t_min > t) {
+        t_min = t;
+        best = k;
+      }
+    }
+  }
+}
+
+template <bool USEBBOX, bool COUNT>
+__global__ __launch_bounds__(TILE) void k_brute(BruteArgs A) {
+  const int n = A.counts[A.depth];
+  if ((int)blockIdx.x * TILE >= n) return;  // uniform per block
+  if (threadIdx.x == 0) atomicMin(&A.trace_t[2 * A.depth], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  const DevScene& S = A.S;
+  const int i = blockIdx.x * TILE + threadIdx.x;
+  bool live = false;
+  f3 o = mk3(0.0f, 0.0f, 0.0f), d = mk3(0.0f, 0.0f, 1.0f);
+  if (i < n) {
+    const float4 q0 = A.paths.p0[i], q1 = A.paths.p1[i];
+    live = fbits(A.paths.p2[i].w) > 0;
+    o = mk3(q0.x, q0.y, q0.z);
+    d = mk3(q1.x, q1.y, q1.z);
+  }
+  // the analytic geoms (src/pathtrace.cu:461-483)
+  float t_min = FLT_MAXV;
+  int geom = -1;
+  if (live) {
+    Ray ray;
+    ray.origin = o;
+    ray.direction = d;
+    ray.isinside = false;
+    ray.sdepth = 0.0f;
+    f3 tmp_i, tmp_n;
+    float t = 0;
+    const f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const bool finite = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
+    for (int g = 0; g < S.num_geoms; g++) {
+      const DevGeom& G = S.geoms[g];
+      if (finite && !geom_may_hit(G, o, inv)) t = -1.0f;
+      else if (G.type == 1) t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
+      else if (G.type == 0) t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+      if (t > 0.0f && t_min > t) {
+        t_min = t;
+        geom = g;
+      }
+    }
+  }
+  // the polygon loop (src/pathtrace.cu:485-576)
+  TraverseCounters cnt{};
+  int best = -1;
+  int objMat = -1;
+  int iterator = 0;  // in vertex indices, like the reference; advances only past shapes whose bbox passed
+  if (S.has_obj) {
+    for (int sh = 0; sh < A.num_shapes; sh++) {
+      const BruteShape B = A.shapes[sh];
+      objMat = fbits(B.hi.w);
+      const int nidx = fbits(B.lo.w);
+      bool take = live;
+      if (USEBBOX) take = live && intersectBbox(o, d, B.lo, B.hi) > -1.0f;
+      const unsigned long long tm = __ballot(take);
+      if (tm) {
+        const int it0 = __shfl(iterator, __builtin_ctzll(tm));
+        if (__all(!take || iterator == it0)) {
+          // every lane that tests this shape starts at the same triangle: scalar triangle fetches
+          const int k0 = __builtin_amdgcn_readfirstlane(it0 / 3);
+          const int nt = nidx / 3;
+          for (int k = k0; k < k0 + nt; k++) {
+            const TriData T = tri_load(S, k);
+            brute_triangle<COUNT>(S, k, T, o, d, t_min, best, take, cnt);
+          }
+        } else {
+          const int nt = nidx / 3;
+          for (int j = 0; j < nt; j++) {
+            const int k = iterator / 3 + j;
+            if (take) {
+              const TriData T = tri_load(S, k);
+              brute_triangle<COUNT>(S, k, T, o, d, t_min, best, true, cnt);
+            }
+          }
+        }
+        if (COUNT && take) cnt.tri += nidx / 3;
+      }
+      if (take) iterator += nidx;
+    }
+  }
+  if (i < n && live) {
+    const int code = best >= 0 ? -(best + 2) : geom;
+    A.hits[i] = make_int2(code, objMat);
+  }
+  if (COUNT) {
+    unsigned int tr = cnt.tri, hi = cnt.hit;
+    for (int off = 32; off > 0; off >>= 1) {
+      tr += __shfl_down(tr, off);
+      hi += __shfl_down(hi, off);
+    }
+    if ((threadIdx.x & 63) == 0) {
+      atomicAdd(&A.counters->tri, (unsigned long long)tr);
+      atomicAdd(&A.counters->hit, (unsigned long long)hi);
+    }
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&A.trace_t[2 * A.depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
+// ---------------------------------------------------------------------------
 // shadeMaterial + scatterRay (src/pathtrace.cu:1885-2100, src/interactions.h) +
 // partialGather, one lane per live path; writes the path in place and the tile's
 // survivor count (or, when sorting, its per-material histogram).
@@ -716,6 +892,10 @@ struct kdpt_ctx {
   std::vector<hipEvent_t>* rec_ev = nullptr;  // when set, launch_iteration records the bounce events here
   double intersect_ms_total = 0;
   long long intersect_launches_total = 0;
+  // enable_kd = 0: brute-force intersect kernel over the OBJ triangles in file order
+  bool brute = false;
+  BruteShape* shapes = nullptr;
+  int num_shapes = 0;
 };
 
 namespace {
@@ -824,6 +1004,9 @@ int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
   c->trace_total = p->trace_total;
   c->wall_khz = p->wall_khz;
   c->sync_debug = p->sync_debug;
+  c->brute = p->brute;
+  c->shapes = p->shapes;
+  c->num_shapes = p->num_shapes;
   int rc;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     kdpt_destroy(c);
@@ -1050,8 +1233,6 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   *out = nullptr;
   kdpt_options o;
   if (opt) o = *opt; else kdpt_default_options(&o);
-  if (!o.enable_kd && sc->has_obj)
-    return fail(KDPT_ERR_UNSUPPORTED, "enable_kd=0 (brute-force pathTraceOneBounce) is not built");
   if (o.viz_kd) return fail(KDPT_ERR_UNSUPPORTED, "viz_kd (pathTraceOneBounceKDbareBoxes) is not built");
   if (o.bounce_cap <= 0) o.bounce_cap = 8;
   if (o.bounce_cap > 30) return fail(KDPT_ERR_ARG, "bounce_cap > 30");
@@ -1062,7 +1243,30 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   // The compact visited-state traversal needs the reference builder's shape:
   // nodes[i].ID == i, root == node 0, node 1 == root's left child, <= 15 levels.
   std::vector<int> level;
-  if (sc->has_obj && sc->num_nodes > 0) {
+  const bool brute = !o.enable_kd && sc->has_obj;
+  if (brute) {
+    // the arrays pathTraceOneBounce reads (src/pathtrace.cu:485-576) must be in bounds
+    if (sc->num_shapes < 1 || !sc->obj_materialOffsets || !sc->obj_polyoffsets || !sc->obj_polysidxflat ||
+        !sc->obj_verts || !sc->obj_norms)
+      return fail(KDPT_ERR_ARG, "enable_kd=0 needs the OBJ arrays (obj_verts, obj_norms, obj_polysidxflat, ...)");
+    long long total = 0;
+    for (int i = 0; i < sc->num_shapes; i++) {
+      if (sc->obj_polyoffsets[i] < 0 || sc->obj_polyoffsets[i] % 3)
+        return fail(KDPT_ERR_UNSUPPORTED, "OBJ shapes must be triangulated (index counts multiple of 3)");
+      if (sc->obj_materialOffsets[i] < 0 || sc->obj_materialOffsets[i] >= sc->num_materials)
+        return fail(KDPT_ERR_ARG, "obj_materialOffsets out of range");
+      total += sc->obj_polyoffsets[i];
+    }
+    if (total != sc->polyidxcount) return fail(KDPT_ERR_ARG, "obj_polyoffsets do not sum to polyidxcount");
+    for (int j = 0; j < sc->polyidxcount; j++) {
+      const long long v = sc->obj_polysidxflat[j];
+      if (v < 0 || 3 * v + 2 >= sc->num_obj_verts || 3 * v + 2 >= sc->num_obj_norms)
+        return fail(KDPT_ERR_ARG, "OBJ vertex index out of range (vertex or normal array)");
+    }
+    if (o.use_bbox && (!sc->obj_bboxes || sc->num_bbox_floats < sc->num_shapes + 5))
+      return fail(KDPT_ERR_ARG, "use_bbox needs obj_bboxes[num_shapes + 5]");
+  }
+  if (sc->has_obj && sc->num_nodes > 0 && !brute) {
     const kdpt_node_bare* N = sc->nodes;
     int root = -1;
     for (int i = 0; i < sc->num_nodes; i++)
@@ -1169,7 +1373,7 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   c->S.num_nodes = sc->has_obj ? sc->num_nodes : 0;
   c->S.root = 0;
   c->S.n0_left = c->S.n0_right = c->S.n1_left = c->S.n1_right = -1;
-  if (sc->has_obj && sc->num_nodes > 0) {
+  if (sc->has_obj && sc->num_nodes > 0 && !brute) {
     const int nn = sc->num_nodes, nt = sc->num_tris;
     std::vector<int4> nodes(4 * (size_t)nn);
     std::vector<float4> tv(nt), e1(nt), e2(nt), n0(nt), n1(nt), n2(nt);
@@ -1224,6 +1428,54 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
       c->S.n1_left = sc->nodes[1].leftID;
       c->S.n1_right = sc->nodes[1].rightID;
     }
+  } else if (brute) {
+    // pathTraceOneBounce's triangles: the file-order OBJ triangles (vertex/normal gathers done here
+    // once; the values are the ones the reference's kernel gathers per test)
+    const int nt = sc->polyidxcount / 3;
+    std::vector<float4> tv(nt), e1(nt), e2(nt), n0(nt), n1(nt), n2(nt);
+    for (int k = 0; k < nt; k++) {
+      const int* ix = sc->obj_polysidxflat + 3 * (size_t)k;
+      const float* a = sc->obj_verts + 3 * (size_t)ix[0];
+      const float* b = sc->obj_verts + 3 * (size_t)ix[1];
+      const float* cc = sc->obj_verts + 3 * (size_t)ix[2];
+      tv[k] = make_float4(a[0], a[1], a[2], 0.0f);
+      e1[k] = make_float4(b[0] - a[0], b[1] - a[1], b[2] - a[2], 0.0f);
+      e2[k] = make_float4(cc[0] - a[0], cc[1] - a[1], cc[2] - a[2], 0.0f);
+      const float* na = sc->obj_norms + 3 * (size_t)ix[0];
+      const float* nb = sc->obj_norms + 3 * (size_t)ix[1];
+      const float* nc = sc->obj_norms + 3 * (size_t)ix[2];
+      n0[k] = make_float4(na[0], na[1], na[2], 0.0f);
+      n1[k] = make_float4(nb[0], nb[1], nb[2], 0.0f);
+      n2[k] = make_float4(nc[0], nc[1], nc[2], 0.0f);
+    }
+    std::vector<BruteShape> shp(sc->num_shapes);
+    for (int i = 0; i < sc->num_shapes; i++) {
+      // glm::vec3(obj_polysbboxes[i] - 0.01, ...): double arithmetic, rounded to float by the constructor
+      const float* bb = sc->obj_bboxes;
+      float l[3] = {0, 0, 0}, h[3] = {0, 0, 0};
+      if (o.use_bbox)
+        for (int k = 0; k < 3; k++) {
+          l[k] = (float)((double)bb[i + k] - 0.01);
+          h[k] = (float)((double)bb[i + 3 + k] + 0.01);
+        }
+      shp[i].lo = make_float4(l[0], l[1], l[2], ibits(sc->obj_polyoffsets[i]));
+      shp[i].hi = make_float4(h[0], h[1], h[2], ibits(sc->obj_materialOffsets[i]));
+    }
+    float4 *dtv, *de1, *de2, *dn0, *dn1, *dn2;
+    if ((rc = dupload(c, &dtv, tv.data(), nt)) || (rc = dupload(c, &de1, e1.data(), nt)) ||
+        (rc = dupload(c, &de2, e2.data(), nt)) || (rc = dupload(c, &dn0, n0.data(), nt)) ||
+        (rc = dupload(c, &dn1, n1.data(), nt)) || (rc = dupload(c, &dn2, n2.data(), nt)) ||
+        (rc = dupload(c, &c->shapes, shp.data(), shp.size())))
+      return bail(rc);
+    c->S.tv0 = dtv;
+    c->S.te1 = de1;
+    c->S.te2 = de2;
+    c->S.tn0 = dn0;
+    c->S.tn1 = dn1;
+    c->S.tn2 = dn2;
+    c->S.num_nodes = 0;
+    c->num_shapes = sc->num_shapes;
+    c->brute = true;
   } else {
     c->S.has_obj = 0;
   }
@@ -1671,14 +1923,46 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     t.depth = depth;
     t.counters = c0->counters;
     t.trace_t = c0->trace_t;
-    for (int b = 0; b < nb; b++) {
-      kdpt_ctx* c = cs[b];
-      hipLaunchKernelGGL(k_geoms, dim3(c->ntiles), dim3(TILE), 0, st, c->S, c->buf[c->cur], c->counts, depth,
-                         c->geomhit);
+    if (c0->brute) {
+      for (int b = 0; b < nb; b++) {
+        kdpt_ctx* c = cs[b];
+        BruteArgs ba;
+        ba.S = c->S;
+        ba.paths = c->buf[c->cur];
+        ba.counts = c->counts;
+        ba.depth = depth;
+        ba.hits = c->hits;
+        ba.shapes = c->shapes;
+        ba.num_shapes = c->num_shapes;
+        ba.counters = c0->counters;
+        ba.trace_t = c0->trace_t;
+        const dim3 g(c->ntiles), bl(TILE);
+        if (c->opt.use_bbox) {
+          if (count) hipLaunchKernelGGL((k_brute<true, true>), g, bl, 0, st, ba);
+          else hipLaunchKernelGGL((k_brute<true, false>), g, bl, 0, st, ba);
+        } else {
+          if (count) hipLaunchKernelGGL((k_brute<false, true>), g, bl, 0, st, ba);
+          else hipLaunchKernelGGL((k_brute<false, false>), g, bl, 0, st, ba);
+        }
+        HIP_TRY(hipGetLastError());
+        if (c0->sync_debug) {
+          BruteShape h0;
+          HIP_TRY(hipMemcpy(&h0, c->shapes, sizeof h0, hipMemcpyDeviceToHost));
+          fprintf(stderr, "[kdpt] brute depth %d use_bbox %d shapes %d lo %g %g %g hi %g %g %g n %d mat %d\n", depth,
+                  c->opt.use_bbox, c->num_shapes, h0.lo.x, h0.lo.y, h0.lo.z, h0.hi.x, h0.hi.y, h0.hi.z, fbits(h0.lo.w),
+                  fbits(h0.hi.w));
+        }
+      }
+    } else {
+      for (int b = 0; b < nb; b++) {
+        kdpt_ctx* c = cs[b];
+        hipLaunchKernelGGL(k_geoms, dim3(c->ntiles), dim3(TILE), 0, st, c->S, c->buf[c->cur], c->counts, depth,
+                           c->geomhit);
+        HIP_TRY(hipGetLastError());
+      }
+      launch_trace(c0, t, count, st);
       HIP_TRY(hipGetLastError());
     }
-    launch_trace(c0, t, count, st);
-    HIP_TRY(hipGetLastError());
     if (c0->sync_debug) {
       fprintf(stderr, "[kdpt] trace depth %d launched (grid %d, mode %d, lds %zu, batch %d)\n", depth,
               c0->trace_grid, c0->tree_mode, c0->tree_lds, nb);
@@ -1706,7 +1990,8 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       a.total_segments = c->total_segments;
       a.trace_t = c0->trace_t;
       a.trace_total = b == 0 ? c->trace_total : nullptr;
-      if (c->opt.short_stack) launch_shade_h<true>(c, a, compact, sort, st);
+      // hit point offset: 1e-4 for the hybrid traversal and the brute-force kernel, 1e-5 for traverseKDbare
+      if (c->opt.short_stack || c->brute) launch_shade_h<true>(c, a, compact, sort, st);
       else launch_shade_h<false>(c, a, compact, sort, st);
       HIP_TRY(hipGetLastError());
       if (compact || sort) {

@@ -15,6 +15,8 @@
 // Float semantics: compiled with -ffp-contract=off, no fast-math; every float
 // and double operation is the one the reference spells (incl. its float ->
 // double promotions), libm calls go to the same glibc the reference links.
+#include <algorithm>
+#include <cfloat>
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
@@ -41,6 +43,9 @@ struct kdpt_scene_data {
   std::vector<kdpt_tri_bare> tris;
   std::vector<int> obj_materialOffsets;
   bool has_obj = false;
+  // the raw OBJ arrays of the brute-force mode (src/scene.cpp:603-712), in triangle-soup form
+  std::vector<float> obj_verts, obj_norms, obj_bboxes;
+  std::vector<int> obj_polyoffsets, obj_polysidxflat;
 };
 
 namespace {
@@ -823,6 +828,46 @@ void build_camera(const kdpt_scene_desc& d, kdpt_camera& cam) {
   memcpy(cam.position, &cp, 12);
 }
 
+// The OBJ arrays Scene::loadObj keeps for the brute-force kernel (src/scene.cpp:603-712), from the
+// per-triangle soup: vertex index 3*t+k holds triangle t's k-th vertex and its vertex-index-gathered
+// normal, so every value pathTraceOneBounce reads is the one the reference reads.  Shapes are the runs of
+// shape_of_tri.  Bboxes as the reference's loop computes them: first vertex of each triangle only, max
+// initialised to 0, stored at [iterator .. iterator+5] (the buffer is sized so that stays in bounds).
+void obj_arrays(const kdpt_scene_desc& d, kdpt_scene_data& sd) {
+  const int nt = d.ntri, nsh = d.num_shapes;
+  sd.obj_verts.assign(d.verts9, d.verts9 + 9 * (size_t)nt);
+  sd.obj_norms.assign(d.norms9, d.norms9 + 9 * (size_t)nt);
+  sd.obj_polysidxflat.resize(3 * (size_t)nt);
+  for (int j = 0; j < 3 * nt; j++) sd.obj_polysidxflat[j] = j;
+  sd.obj_polyoffsets.assign(std::max(nsh, 0), 0);
+  for (int t = 0; t < nt; t++) {
+    const int sh = d.shape_of_tri[t];
+    if (sh >= 0 && sh < nsh) sd.obj_polyoffsets[sh] += 3;
+  }
+  int nb = 6 * nsh, it = 0;
+  for (int i = 0; i < nsh; i++) {
+    nb = std::max(nb, it + 6);
+    it += sd.obj_polyoffsets[i];
+  }
+  sd.obj_bboxes.assign(std::max(nb, nsh + 5), 0.0f);
+  int iterator = 0;
+  for (int i = 0; i < nsh; i++) {
+    float minx = FLT_MAX, maxx = 0.0f, miny = FLT_MAX, maxy = 0.0f, minz = FLT_MAX, maxz = 0.0f;
+    for (int j = iterator; j < iterator + sd.obj_polyoffsets[i]; j += 3) {
+      const float* v = sd.obj_verts.data() + 3 * (size_t)sd.obj_polysidxflat[j];
+      if (v[0] < minx) minx = v[0];
+      if (v[0] > maxx) maxx = v[0];
+      if (v[1] < miny) miny = v[1];
+      if (v[1] > maxy) maxy = v[1];
+      if (v[2] < minz) minz = v[2];
+      if (v[2] > maxz) maxz = v[2];
+    }
+    float* b = sd.obj_bboxes.data() + iterator;
+    b[0] = minx; b[1] = miny; b[2] = minz; b[3] = maxx; b[4] = maxy; b[5] = maxz;
+    iterator += sd.obj_polyoffsets[i];
+  }
+}
+
 }  // namespace
 
 extern "C" {
@@ -860,6 +905,7 @@ int kdpt_scene_build(const kdpt_scene_desc* d, kdpt_scene_data** out) {
     build_kd(d->verts9, d->norms9, d->shape_of_tri, d->ntri, d->kd_max_depth > 0 ? d->kd_max_depth : 13,
              sd->nodes, sd->tris);
     sd->has_obj = true;
+    obj_arrays(*d, *sd);
   }
   *out = sd.release();
   return KDPT_OK;
@@ -916,6 +962,15 @@ int kdpt_scene_view(const kdpt_scene_data* sd, kdpt_scene* o) {
   o->num_tris = (int)sd->tris.size();
   o->obj_materialOffsets = sd->obj_materialOffsets.data();
   o->num_shapes = (int)sd->obj_materialOffsets.size();
+  o->obj_verts = sd->obj_verts.data();
+  o->num_obj_verts = (int)sd->obj_verts.size();
+  o->obj_norms = sd->obj_norms.data();
+  o->num_obj_norms = (int)sd->obj_norms.size();
+  o->obj_polyoffsets = sd->obj_polyoffsets.data();
+  o->obj_polysidxflat = sd->obj_polysidxflat.data();
+  o->polyidxcount = (int)sd->obj_polysidxflat.size();
+  o->obj_bboxes = sd->obj_bboxes.data();
+  o->num_bbox_floats = (int)sd->obj_bboxes.size();
   return KDPT_OK;
 }
 

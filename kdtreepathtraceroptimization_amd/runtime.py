@@ -69,7 +69,11 @@ class Scene(C.Structure):
     _fields_ = [("camera", Camera), ("traceDepth", C.c_int), ("geoms", C.POINTER(Geom)), ("num_geoms", C.c_int),
                 ("materials", C.POINTER(Material)), ("num_materials", C.c_int), ("has_obj", C.c_int),
                 ("nodes", C.POINTER(NodeBare)), ("num_nodes", C.c_int), ("tris", C.POINTER(TriBare)),
-                ("num_tris", C.c_int), ("obj_materialOffsets", C.POINTER(C.c_int)), ("num_shapes", C.c_int)]
+                ("num_tris", C.c_int), ("obj_materialOffsets", C.POINTER(C.c_int)), ("num_shapes", C.c_int),
+                ("obj_verts", C.POINTER(C.c_float)), ("num_obj_verts", C.c_int), ("obj_norms", C.POINTER(C.c_float)),
+                ("num_obj_norms", C.c_int), ("obj_polyoffsets", C.POINTER(C.c_int)),
+                ("obj_polysidxflat", C.POINTER(C.c_int)), ("polyidxcount", C.c_int),
+                ("obj_bboxes", C.POINTER(C.c_float)), ("num_bbox_floats", C.c_int)]
 
 
 class Options(C.Structure):

@@ -622,6 +622,71 @@ static void traverseKD(const orc_scene *s, ray_t ray, v3 *bary, hitrec_t *h, uns
 #undef VIS
 }
 
+/* intersectBbox, src/interactions.h:136-165 (min/max as in intersectAABBarrays) */
+static inline float intersectBbox(v3 origin, v3 direction, v3 mn, v3 mx) {
+    v3 invdir = V3(1.0f / direction.x, 1.0f / direction.y, 1.0f / direction.z);
+    float v1 = (mn.x - origin.x) * invdir.x;
+    float v2 = (mx.x - origin.x) * invdir.x;
+    float v3_ = (mn.y - origin.y) * invdir.y;
+    float v4_ = (mx.y - origin.y) * invdir.y;
+    float v5 = (mn.z - origin.z) * invdir.z;
+    float v6 = (mx.z - origin.z) * invdir.z;
+    float dmin = std_max(std_max(std_min(v1, v2), std_min(v3_, v4_)), std_min(v5, v6));
+    float dmax = std_min(std_min(std_max(v1, v2), std_max(v3_, v4_)), std_max(v5, v6));
+    if (dmax < 0) return dmax;
+    if (dmin > dmax) return dmax;
+    return dmin;
+}
+
+/* The polygon loop of pathTraceOneBounce (enable_kd == false), src/pathtrace.cu:485-576: every
+ * triangle of every OBJ shape in file order, optionally behind the shape's bbox test.  Kept as the
+ * reference spells it: the bbox is read at obj_polysbboxes[i .. i+5] (shape index, not 6*i), the
+ * double +-0.01 margin is rounded to float by glm::vec3's converting constructor, `iterator` only
+ * advances for shapes whose bbox test passed, and objMaterialIdx ends as the LAST shape's offset. */
+static void bruteForceObj(const orc_scene *s, ray_t ray, int usebbox, hitrec_t *h, counters_t *cnt) {
+    int iterator = 0;
+    int objMaterialIdx = -1;
+    const float *bb = s->obj_bboxes;
+    for (int i = 0; i < s->num_shapes; i++) {
+        objMaterialIdx = s->obj_materialOffsets[i];
+        float T;
+        if (usebbox) {
+            v3 mn = V3((float)((double)bb[i] - 0.01), (float)((double)bb[i + 1] - 0.01), (float)((double)bb[i + 2] - 0.01));
+            v3 mx = V3((float)((double)bb[i + 3] + 0.01), (float)((double)bb[i + 4] + 0.01), (float)((double)bb[i + 5] + 0.01));
+            T = intersectBbox(ray.origin, ray.direction, mn, mx);
+        } else {
+            T = 0;
+        }
+        if (T > -1.0f) {
+            for (int j = iterator; j < iterator + s->obj_polyoffsets[i]; j += 3) {
+                int p1 = 3 * s->obj_polysidxflat[j], p2 = 3 * s->obj_polysidxflat[j + 1], p3 = 3 * s->obj_polysidxflat[j + 2];
+                const float *V = s->obj_verts, *N = s->obj_norms;
+                v3 v1 = V3(V[p1], V[p1 + 1], V[p1 + 2]), v2 = V3(V[p2], V[p2 + 1], V[p2 + 2]), v3_ = V3(V[p3], V[p3 + 1], V[p3 + 2]);
+                v3 n1 = V3(N[p1], N[p1 + 1], N[p1 + 2]), n2 = V3(N[p2], N[p2 + 1], N[p2 + 2]), n3 = V3(N[p3], N[p3 + 1], N[p3 + 2]);
+                v3 bary = V3(0.0f, 0.0f, 0.0f);
+                cnt->tri++;
+                int intersected = intersectRayTriangle(ray.origin, ray.direction, v1, v2, v3_, &bary);
+                if (!intersected) continue;
+                cnt->hit++;
+                v3 hit = vadd(ray.origin, vscale(ray.direction, bary.z));
+                float w0 = 1 - bary.x - bary.y;
+                v3 norm = vnormalize(vadd(vadd(vscale(n1, w0), vscale(n2, bary.x)), vscale(n3, bary.y)));
+                hit = vadd(hit, vscale(norm, 0.0001f));
+                float t = vdistance(ray.origin, hit);
+                if (t > 0.0f && h->t_min > t) {
+                    h->t_min = t;
+                    h->hit_geom_index = s->obj_materialOffsets[i];
+                    h->intersect_point = hit;
+                    h->normal = norm;
+                    h->obj_intersect = 1;
+                }
+            }
+            iterator += s->obj_polyoffsets[i];
+        }
+    }
+    h->objMaterialIdx = objMaterialIdx;
+}
+
 /* ------------------------------------------------------------------ */
 /* Kernels as host loops                                                */
 /* ------------------------------------------------------------------ */
@@ -724,7 +789,10 @@ static void traceOneBounce(const orc_scene *s, const orc_opts *o, int depth, int
                 }
             }
             v3 bary = V3(0, 0, 0);
-            if (s->has_obj) traverseKD(s, ray, &bary, &h, visited, o->shortstack, nmat, &cnt);
+            if (s->has_obj) {
+                if (o->enable_kd) traverseKD(s, ray, &bary, &h, visited, o->shortstack, nmat, &cnt);
+                else bruteForceObj(s, ray, o->usebbox, &h, &cnt);
+            }
             orc_isect *I = &isects[path_index];
             if (h.hit_geom_index == -1) {
                 I->t = -1.0f;
@@ -913,6 +981,8 @@ void orc_default_opts(orc_opts *o) {
     o->compaction = 1;
     o->shortstack = 1;
     o->bounce_cap = 8;
+    o->enable_kd = 1;
+    o->usebbox = 0;
 }
 
 int orc_render(const orc_scene *s, const orc_opts *o, int iter_first, int iter_count, float *image,
@@ -1730,6 +1800,48 @@ void orc_free_desc(orc_scene_desc *d) {
     memset(d, 0, sizeof *d);
 }
 
+/* The raw OBJ arrays Scene::loadObj keeps for the brute-force kernel (src/scene.cpp:603-712), from
+ * the per-triangle soup: vertex index 3*t+k holds triangle t's k-th vertex (and its vertex-index-
+ * gathered normal), so every value the kernel reads is the one the reference reads.  Shapes are the
+ * runs of shape_of_tri.  The bboxes follow the reference's loop: first vertex of each triangle only,
+ * max initialised to 0, stored at [iterator .. iterator+5] (in-bounds here: the buffer is sized for it). */
+static void obj_arrays(const orc_scene_desc *d, orc_scene *out) {
+    int nt = d->ntri, nsh = d->num_shapes;
+    out->polyidxcount = 3 * nt;
+    out->obj_verts = (float *)malloc(sizeof(float) * 9 * (size_t)nt);
+    out->obj_norms = (float *)malloc(sizeof(float) * 9 * (size_t)nt);
+    memcpy(out->obj_verts, d->verts9, sizeof(float) * 9 * (size_t)nt);
+    memcpy(out->obj_norms, d->norms9, sizeof(float) * 9 * (size_t)nt);
+    out->obj_polysidxflat = (int *)malloc(sizeof(int) * 3 * (size_t)nt);
+    for (int j = 0; j < 3 * nt; j++) out->obj_polysidxflat[j] = j;
+    out->obj_polyoffsets = (int *)calloc((size_t)(nsh > 0 ? nsh : 1), sizeof(int));
+    for (int t = 0; t < nt; t++) {
+        int sh = d->shape_of_tri[t];
+        if (sh >= 0 && sh < nsh) out->obj_polyoffsets[sh] += 3;
+    }
+    int nb = 6 * nsh, it = 0;
+    for (int i = 0; i < nsh; i++) { if (it + 6 > nb) nb = it + 6; it += out->obj_polyoffsets[i]; }
+    if (nsh + 5 > nb) nb = nsh + 5;
+    out->num_bbox_floats = nb;
+    out->obj_bboxes = (float *)calloc((size_t)nb, sizeof(float));
+    int iterator = 0;
+    for (int i = 0; i < nsh; i++) {
+        float minx = FLT_MAX, maxx = 0.0f, miny = FLT_MAX, maxy = 0.0f, minz = FLT_MAX, maxz = 0.0f;
+        for (int j = iterator; j < iterator + out->obj_polyoffsets[i]; j += 3) {
+            const float *v = out->obj_verts + 3 * out->obj_polysidxflat[j];
+            if (v[0] < minx) minx = v[0];
+            if (v[0] > maxx) maxx = v[0];
+            if (v[1] < miny) miny = v[1];
+            if (v[1] > maxy) maxy = v[1];
+            if (v[2] < minz) minz = v[2];
+            if (v[2] > maxz) maxz = v[2];
+        }
+        float *b = out->obj_bboxes + iterator;
+        b[0] = minx; b[1] = miny; b[2] = minz; b[3] = maxx; b[4] = maxy; b[5] = maxz;
+        iterator += out->obj_polyoffsets[i];
+    }
+}
+
 int orc_build_scene(const orc_scene_desc *d, orc_scene *out) {
     memset(out, 0, sizeof *out);
     orc_camera *cam = &out->camera;
@@ -1796,6 +1908,7 @@ int orc_build_scene(const orc_scene_desc *d, orc_scene *out) {
         orc_build_kd(d->verts9, d->norms9, d->shape_of_tri, d->ntri, 13, &out->nodes, &out->num_nodes, &out->tris,
                      &out->num_tris);
         out->has_obj = 1;
+        obj_arrays(d, out);
     }
     return 0;
 }
@@ -1813,5 +1926,6 @@ int orc_load_scene(const char *scene_path, const char *obj_path, int res_w, int 
 
 void orc_free_scene(orc_scene *s) {
     free(s->geoms); free(s->materials); free(s->obj_materialOffsets); free(s->nodes); free(s->tris);
+    free(s->obj_verts); free(s->obj_norms); free(s->obj_polysidxflat); free(s->obj_polyoffsets); free(s->obj_bboxes);
     memset(s, 0, sizeof *s);
 }

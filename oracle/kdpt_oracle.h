@@ -112,6 +112,12 @@ typedef struct {
     int num_nodes, num_tris;
     orc_node *nodes;
     orc_tri *tris;
+    /* enable_kd == false (pathTraceOneBounce): the raw OBJ arrays, src/scene.cpp:603-712 */
+    int polyidxcount;
+    float *obj_verts, *obj_norms;
+    int *obj_polysidxflat, *obj_polyoffsets;
+    float *obj_bboxes;
+    int num_bbox_floats;
 } orc_scene;
 
 /* Flags of pathtrace() (src/pathtrace.h:6-21, defaults src/main.cpp:35-60). */
@@ -125,6 +131,8 @@ typedef struct {
     int compaction;      /* 1 */
     int shortstack;      /* 1 */
     int bounce_cap;      /* 8 == the reference's hard-coded `depth > 7` (src/pathtrace.cu:2608) */
+    int enable_kd;       /* 1; 0 = brute-force pathTraceOneBounce (src/pathtrace.cu:402-628) */
+    int usebbox;         /* 0; brute force only: per-shape bbox test first */
 } orc_opts;
 
 typedef struct {

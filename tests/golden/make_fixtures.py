@@ -28,7 +28,10 @@ from kdtreepathtraceroptimization_amd.runtime import MATERIAL_DTYPE  # noqa: E40
 
 REF = "/root/reference"
 SCENES = {"cornell": "scenes/cornell.txt", "cornell8": "scenes/cornell8.txt"}
-MESHES = {"sphere_low_1": "scenes/sphere_low_1.obj", "dragon_5": "scenes/dragon_5.obj"}
+MESHES = {"sphere_low_1": "scenes/sphere_low_1.obj", "dragon_5": "scenes/dragon_5.obj",
+          # the other meshes of the reference's benchmark table (presentation/resultformat*.py) that exist
+          "dragon_1": "scenes/dragon_1.obj", "dragon_2": "scenes/dragon_2.obj", "dragon_3": "scenes/dragon_3.obj",
+          "dragon_4": "scenes/dragon_4.obj", "sphere_low_8": "scenes/sphere_low_8.obj"}
 
 
 def f32(x):

@@ -44,13 +44,16 @@ class OScene(C.Structure):
     _fields_ = [("camera", OCamera), ("iterations", C.c_int), ("traceDepth", C.c_int), ("num_geoms", C.c_int),
                 ("num_materials", C.c_int), ("geoms", C.POINTER(OGeom)), ("materials", C.POINTER(OMaterial)),
                 ("has_obj", C.c_int), ("num_shapes", C.c_int), ("obj_materialOffsets", C.POINTER(C.c_int)),
-                ("num_nodes", C.c_int), ("num_tris", C.c_int), ("nodes", C.c_void_p), ("tris", C.c_void_p)]
+                ("num_nodes", C.c_int), ("num_tris", C.c_int), ("nodes", C.c_void_p), ("tris", C.c_void_p),
+                ("polyidxcount", C.c_int), ("obj_verts", C.POINTER(C.c_float)), ("obj_norms", C.POINTER(C.c_float)),
+                ("obj_polysidxflat", C.POINTER(C.c_int)), ("obj_polyoffsets", C.POINTER(C.c_int)),
+                ("obj_bboxes", C.POINTER(C.c_float)), ("num_bbox_floats", C.c_int)]
 
 
 class OOpts(C.Structure):
     _fields_ = [("focalLength", C.c_float), ("dofAngle", C.c_float), ("cacherays", C.c_int), ("antialias", C.c_int),
                 ("softness", C.c_float), ("enableSss", C.c_int), ("compaction", C.c_int), ("shortstack", C.c_int),
-                ("bounce_cap", C.c_int)]
+                ("bounce_cap", C.c_int), ("enable_kd", C.c_int), ("usebbox", C.c_int)]
 
 
 class OStats(C.Structure):
