@@ -52,6 +52,8 @@ def parse():
     ap.add_argument("--res", type=int, nargs=2, default=(800, 800))
     ap.add_argument("--depth", type=int, default=8)
     ap.add_argument("--bare", action="store_true", help="traverseKDbare instead of the short-stack hybrid")
+    ap.add_argument("--bounce-cap", type=int, default=8,
+                    help="bounces per iteration (8 = the reference's `depth > 7`; 16 for the C5 stress config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--pipeline", type=int, default=2,
@@ -71,7 +73,7 @@ def cpu_baseline(args):
     seg, t, it = 0, 0.0, 3
     while t < args.cpu_seconds and it < 3 + 64:
         t0 = time.perf_counter()
-        _, st = s.render(it, 1, nthreads=threads, shortstack=0 if args.bare else 1)
+        _, st = s.render(it, 1, nthreads=threads, shortstack=0 if args.bare else 1, bounce_cap=args.bounce_cap)
         t += time.perf_counter() - t0
         seg += st.segments
         it += 1
@@ -99,7 +101,8 @@ def main():
     sd = SceneData.from_description(desc)
     W, H = sd.resolution
     accum = torch.zeros(3 * W * H, dtype=torch.float32, device=f"cuda:{local}")
-    opt = default_options(testing_mode=1, short_stack=0 if args.bare else 1, external_image=accum.data_ptr())
+    opt = default_options(testing_mode=1, short_stack=0 if args.bare else 1, external_image=accum.data_ptr(),
+                          bounce_cap=args.bounce_cap)
     pt = PathTracer(sd, opt, device=local)
 
     from kdtreepathtraceroptimization_amd.distributed import global_iteration, reduce_image
@@ -176,10 +179,12 @@ def main():
         "dtype": "f32",
         "data": "synthetic camera rays over the reference's own scene assets (cornell.txt + dragon_5.obj, "
                 "parsed fixtures under tests/golden); deterministic RNG seeded by iteration",
-        "config": {"workload": f"{args.scene}.txt + {args.mesh}.obj, {W}x{H}, depth {args.depth}, 1 spp per step "
+        "config": {"workload": f"{args.scene}.txt + {args.mesh}.obj, {W}x{H}, depth {args.depth}, "
+                               f"bounce cap {args.bounce_cap}, 1 spp per step "
                                f"per GPU ({args.pipeline} x {args.batch} iterations in flight), "
                                + ("short-stack hybrid KD traversal" if not args.bare else "bare traversal"),
                    "scene": args.scene, "mesh": args.mesh, "resolution": [W, H], "depth": args.depth,
+                   "bounce_cap": args.bounce_cap,
                    "kd_nodes": sd.view.num_nodes, "kd_tri_refs": sd.view.num_tris,
                    "parallelism": f"spp-sharded x{world} + RCCL reduce" if world > 1 else "single GPU"},
         "segments_per_step": seg / (args.steps * world),

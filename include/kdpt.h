@@ -200,6 +200,19 @@ int kdpt_read_image(kdpt_ctx *ctx, float *rgb);
 /* sendImageToPBO (src/pathtrace.cu:69-89) into host uchar4[W*H] (x,y,z,w bytes). */
 int kdpt_write_pbo(kdpt_ctx *ctx, int iter, uint8_t *rgba);
 int kdpt_reset(kdpt_ctx *ctx);
+
+/* ---- Headless output (saveImage, src/main.cpp:1087-1108 + image::savePNG/saveHDR, src/image.cpp:22-45) ---- */
+/* The bytes savePNG encodes: x-flipped, image / samples, glm::clamp(0, 1) * 255.f, (unsigned char). */
+int kdpt_save_rgb8(kdpt_ctx *ctx, float samples, uint8_t *rgb);
+/* image::savePNG / image::saveHDR of the current image (stb_image_write's encoders, restated). */
+int kdpt_save_png(kdpt_ctx *ctx, const char *path, float samples);
+int kdpt_save_hdr(kdpt_ctx *ctx, const char *path, float samples);
+/* The encoders alone (host; no device needed).  *out is malloc'd: release with kdpt_free. */
+int kdpt_png_encode(const uint8_t *rgb, int w, int h, uint8_t **out, size_t *len);
+int kdpt_write_png(const char *path, const uint8_t *rgb, int w, int h);
+int kdpt_hdr_encode(const float *rgb, int w, int h, uint8_t **out, size_t *len);
+int kdpt_write_hdr(const char *path, const float *rgb, int w, int h);
+void kdpt_free(void *p);
 int kdpt_get_stats(kdpt_ctx *ctx, kdpt_stats *st);
 int kdpt_destroy(kdpt_ctx *ctx);
 const char *kdpt_last_error(void);

@@ -53,13 +53,15 @@ def build(force: bool = False, verbose_resources: bool = False) -> str:
         return LIB
     os.makedirs(BUILD, exist_ok=True)
     host_obj = os.path.join(BUILD, "scene_host.o")
+    io_obj = os.path.join(BUILD, "image_io.o")
     dev_obj = os.path.join(BUILD, "kdpt_runtime.o")
     _run(["g++", *COMMON, "-c", os.path.join(CSRC, "scene_host.cpp"), "-o", host_obj])
+    _run(["g++", *COMMON, "-c", os.path.join(CSRC, "image_io.cpp"), "-o", io_obj])
     extra = ["-Rpass-analysis=kernel-resource-usage"] if verbose_resources else []
     _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, *extra, "-c", os.path.join(CSRC, "kdpt_runtime.hip"), "-o", dev_obj],
          log=os.path.join(BUILD, "kdpt_runtime.build.log"))
     tmp = LIB + ".tmp"
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, dev_obj, host_obj])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, dev_obj, host_obj, io_obj])
     os.replace(tmp, LIB)
     return LIB
 

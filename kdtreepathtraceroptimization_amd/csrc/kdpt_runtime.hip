@@ -791,6 +791,24 @@ __global__ void k_pbo(const float* image, int npix, int iter, uchar4* pbo) {
   pbo[index] = make_uchar4((unsigned char)c[0], (unsigned char)c[1], (unsigned char)c[2], 0);
 }
 
+// saveImage (src/main.cpp:1087-1108): x-flip and divide by the sample count, then image::savePNG's
+// bytes (src/image.cpp:22-35): glm::clamp(pix, 0, 1) * 255.f truncated to unsigned char.  `lin`
+// (optional) receives the flipped, divided float image that image::saveHDR writes.
+__global__ void k_save_image(const float* __restrict__ image, int W, int H, float samples, uint8_t* __restrict__ rgb,
+                             float* __restrict__ lin) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= W * H) return;
+  const int y = i / W, X = i - y * W;
+  const size_t src = 3 * ((size_t)(W - 1 - X) + (size_t)y * W);
+#pragma unroll
+  for (int k = 0; k < 3; k++) {
+    const float v = image[src + k] / samples;
+    if (lin) lin[3 * (size_t)i + k] = v;
+    const float cl = glm_min(glm_max(v, 0.0f), 1.0f) * 255.f;
+    rgb[3 * (size_t)i + k] = (uint8_t)cl;
+  }
+}
+
 // debug: unpack the live path array into the reference PathSegment layout
 __global__ void k_unpack(PathBuf src, const int* counts, int depth, kdpt_path_segment* out) {
   const int n = counts[depth];
@@ -1691,6 +1709,54 @@ int kdpt_write_pbo(kdpt_ctx* c, int iter, uint8_t* rgba) {
   HIP_TRY(hipStreamSynchronize(c->stream));
   HIP_TRY(hipFree(d));
   return KDPT_OK;
+}
+
+// The saveImage pixel pass on the device; rgb (host, 3*W*H) and/or lin (host, 3*W*H floats).
+static int save_image_pass(kdpt_ctx* c, float samples, uint8_t* rgb, float* lin) {
+  HIP_TRY(hipSetDevice(c->device));
+  for (auto sl : c->slots) HIP_TRY(hipStreamSynchronize(sl->stream));
+  if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
+  const size_t n3 = 3 * (size_t)c->npix;
+  uint8_t* d_rgb = nullptr;
+  float* d_lin = nullptr;
+  HIP_TRY(hipMalloc((void**)&d_rgb, n3));
+  if (lin && hipMalloc((void**)&d_lin, n3 * sizeof(float)) != hipSuccess) {
+    (void)hipFree(d_rgb);
+    return fail(KDPT_ERR_HIP, "hipMalloc");
+  }
+  hipLaunchKernelGGL(k_save_image, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->image, c->W, c->H,
+                     samples, d_rgb, d_lin);
+  hipError_t e = hipGetLastError();
+  if (e == hipSuccess && rgb) e = hipMemcpyAsync(rgb, d_rgb, n3, hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess && lin) e = hipMemcpyAsync(lin, d_lin, n3 * sizeof(float), hipMemcpyDeviceToHost, c->stream);
+  if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+  (void)hipFree(d_rgb);
+  if (d_lin) (void)hipFree(d_lin);
+  if (e != hipSuccess) return fail(KDPT_ERR_HIP, std::string("save image: ") + hipGetErrorString(e));
+  return KDPT_OK;
+}
+
+int kdpt_save_rgb8(kdpt_ctx* c, float samples, uint8_t* rgb) {
+  if (!c || !rgb) return fail(KDPT_ERR_ARG, "null arg");
+  return save_image_pass(c, samples, rgb, nullptr);
+}
+
+int kdpt_save_png(kdpt_ctx* c, const char* path, float samples) {
+  if (!c || !path) return fail(KDPT_ERR_ARG, "null arg");
+  std::vector<uint8_t> rgb(3 * (size_t)c->npix);
+  int rc = save_image_pass(c, samples, rgb.data(), nullptr);
+  if (rc) return rc;
+  rc = kdpt_write_png(path, rgb.data(), c->W, c->H);
+  return rc ? fail(rc, std::string("cannot write ") + path) : KDPT_OK;
+}
+
+int kdpt_save_hdr(kdpt_ctx* c, const char* path, float samples) {
+  if (!c || !path) return fail(KDPT_ERR_ARG, "null arg");
+  std::vector<float> lin(3 * (size_t)c->npix);
+  int rc = save_image_pass(c, samples, nullptr, lin.data());
+  if (rc) return rc;
+  rc = kdpt_write_hdr(path, lin.data(), c->W, c->H);
+  return rc ? fail(rc, std::string("cannot write ") + path) : KDPT_OK;
 }
 
 int kdpt_get_stats(kdpt_ctx* c, kdpt_stats* st) {

@@ -110,6 +110,8 @@ EXPORTS = [
     "kdpt_read_image", "kdpt_write_pbo", "kdpt_reset", "kdpt_get_stats", "kdpt_destroy", "kdpt_last_error",
     "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_wave_profile", "kdpt_selftest_math", "kdpt_selftest_rng",
     "kdpt_selftest_fresnel", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
+    "kdpt_save_rgb8", "kdpt_save_png", "kdpt_save_hdr", "kdpt_png_encode", "kdpt_write_png", "kdpt_hdr_encode",
+    "kdpt_write_hdr", "kdpt_free",
 ]
 
 _lib = None
@@ -153,6 +155,15 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_scene_build.argtypes = [P(SceneDesc), P(C.c_void_p)]
     lib.kdpt_scene_view.argtypes = [C.c_void_p, P(Scene)]
     lib.kdpt_scene_free.argtypes = [C.c_void_p]
+    lib.kdpt_save_rgb8.argtypes = [C.c_void_p, C.c_float, P(C.c_uint8)]
+    lib.kdpt_save_png.argtypes = [C.c_void_p, C.c_char_p, C.c_float]
+    lib.kdpt_save_hdr.argtypes = [C.c_void_p, C.c_char_p, C.c_float]
+    lib.kdpt_png_encode.argtypes = [P(C.c_uint8), C.c_int, C.c_int, P(P(C.c_uint8)), P(C.c_size_t)]
+    lib.kdpt_write_png.argtypes = [C.c_char_p, P(C.c_uint8), C.c_int, C.c_int]
+    lib.kdpt_hdr_encode.argtypes = [P(C.c_float), C.c_int, C.c_int, P(P(C.c_uint8)), P(C.c_size_t)]
+    lib.kdpt_write_hdr.argtypes = [C.c_char_p, P(C.c_float), C.c_int, C.c_int]
+    lib.kdpt_free.argtypes = [C.c_void_p]
+    lib.kdpt_free.restype = None
     _lib = lib
     return lib
 
@@ -296,6 +307,30 @@ class SceneData:
             pass
 
 
+def _encoded(fn, ptr, w, h, what) -> bytes:
+    out = C.POINTER(C.c_uint8)()
+    n = C.c_size_t()
+    _check(fn(ptr, int(w), int(h), C.byref(out), C.byref(n)), what)
+    try:
+        return C.string_at(out, n.value)
+    finally:
+        load_library().kdpt_free(out)
+
+
+def png_encode(rgb: np.ndarray) -> bytes:
+    """PNG bytes of an (H, W, 3) uint8 image, as stb_image_write's stbi_write_png encodes them."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.uint8)
+    h, w = rgb.shape[:2]
+    return _encoded(load_library().kdpt_png_encode, rgb.ctypes.data_as(C.POINTER(C.c_uint8)), w, h, "kdpt_png_encode")
+
+
+def hdr_encode(rgb: np.ndarray) -> bytes:
+    """Radiance .hdr bytes of an (H, W, 3) float32 image, as stb_image_write's stbi_write_hdr writes them."""
+    rgb = np.ascontiguousarray(rgb, dtype=np.float32)
+    h, w = rgb.shape[:2]
+    return _encoded(load_library().kdpt_hdr_encode, _fptr(rgb), w, h, "kdpt_hdr_encode")
+
+
 def default_options(**overrides) -> Options:
     o = Options()
     load_library().kdpt_default_options(C.byref(o))
@@ -347,6 +382,21 @@ class PathTracer:
 
     def reset(self):
         _check(self.lib.kdpt_reset(self._ctx), "kdpt_reset")
+
+    def save_rgb8(self, samples: float) -> np.ndarray:
+        """saveImage's bytes (src/main.cpp:1087-1108, src/image.cpp:22-35), computed on the GPU."""
+        out = np.empty((self.height, self.width, 3), dtype=np.uint8)
+        _check(self.lib.kdpt_save_rgb8(self._ctx, float(samples), out.ctypes.data_as(C.POINTER(C.c_uint8))),
+               "kdpt_save_rgb8")
+        return out
+
+    def save_png(self, path: str, samples: float):
+        """image::savePNG of the current image: the PNG the reference writes (stb encoder, restated)."""
+        _check(self.lib.kdpt_save_png(self._ctx, os.fsencode(path), float(samples)), "kdpt_save_png")
+
+    def save_hdr(self, path: str, samples: float):
+        """image::saveHDR (Radiance RGBE, stb encoder restated)."""
+        _check(self.lib.kdpt_save_hdr(self._ctx, os.fsencode(path), float(samples)), "kdpt_save_hdr")
 
     def stats(self) -> Stats:
         s = Stats()

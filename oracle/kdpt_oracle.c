@@ -1929,3 +1929,20 @@ void orc_free_scene(orc_scene *s) {
     free(s->obj_verts); free(s->obj_norms); free(s->obj_polysidxflat); free(s->obj_polyoffsets); free(s->obj_bboxes);
     memset(s, 0, sizeof *s);
 }
+
+/* saveImage (src/main.cpp:1087-1108) + image::savePNG's byte conversion (src/image.cpp:22-35):
+ * img.setPixel(width-1-x, y, pix / samples); glm::clamp(p, 0, 1) * 255.f; (unsigned char).
+ * lin (optional) receives the flipped, divided floats (what image::saveHDR writes). */
+void orc_save_image(const float *image, int W, int H, float samples, unsigned char *rgb, float *lin) {
+    for (int x = 0; x < W; x++)
+        for (int y = 0; y < H; y++) {
+            int src = 3 * (x + y * W), dst = 3 * ((W - 1 - x) + y * W);
+            for (int k = 0; k < 3; k++) {
+                float v = image[src + k] / samples;
+                if (lin) lin[dst + k] = v;
+                float mx = v > 0.0f ? v : 0.0f;       /* glm::max(x, y) = x > y ? x : y */
+                float cl = mx < 1.0f ? mx : 1.0f;     /* glm::min(x, y) = x < y ? x : y */
+                if (rgb) rgb[dst + k] = (unsigned char)(cl * 255.f);
+            }
+        }
+}

@@ -218,6 +218,9 @@ int orc_paths_after(const orc_scene *s, const orc_opts *o, int iter, int stop_de
  * out[8]=obj_intersect out[9]=objMaterialIdx out[10..12]=aabb/tri/hit tests out[13]=leaves visited (size > 0). */
 int orc_trace_ray(const orc_scene *s, const float *origin, const float *direction, int hybrid, double *out);
 
+/* saveImage + image::savePNG's bytes (src/main.cpp:1087-1108, src/image.cpp:22-35); lin may be NULL. */
+void orc_save_image(const float *image, int W, int H, float samples, unsigned char *rgb, float *lin);
+
 /* Device-math known answers shared with the HIP tests. */
 unsigned int orc_utilhash(unsigned int a);
 float orc_u01_sequence(int iter, int index, int depth, int k); /* k-th uniform */

@@ -102,6 +102,7 @@ def lib():
         L.orc_u01_array.argtypes = [P(C.c_int), C.c_int, C.c_int, P(C.c_float)]
         L.orc_fresnel_array.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
         L.orc_trace_ray.argtypes = [P(OScene), P(C.c_float), P(C.c_float), C.c_int, P(C.c_double)]
+        L.orc_save_image.argtypes = [P(C.c_float), C.c_int, C.c_int, C.c_float, P(C.c_uint8), P(C.c_float)]
         _lib = L
     return _lib
 
@@ -268,3 +269,14 @@ def fresnel(cosines: np.ndarray, ior: float):
     f = np.empty_like(c)
     lib().orc_fresnel_array(_fp(c), len(c), float(np.float32(ior)), _fp(f))
     return f
+
+
+def save_image(image: np.ndarray, samples: float):
+    """saveImage's bytes and the flipped/divided floats (oracle restatement)."""
+    image = np.ascontiguousarray(image, np.float32)
+    h, w = image.shape[:2]
+    rgb = np.empty((h, w, 3), np.uint8)
+    lin = np.empty((h, w, 3), np.float32)
+    lib().orc_save_image(_fp(image), w, h, float(np.float32(samples)), rgb.ctypes.data_as(C.POINTER(C.c_uint8)),
+                         _fp(lin))
+    return rgb, lin
