@@ -12,14 +12,15 @@ across ranks (rank r renders global iterations r+1, r+1+N, ...: weak scaling) an
 float3 accumulation images are summed on rank 0 with one RCCL reduce over xGMI inside
 the timed region.
 
-Roofline: the dominant kernel is the intersect kernel (k_trace: analytic geoms + KD traversal,
-the reference's pathTraceOneBounce*).  HBM-bound; algorithmic bytes per segment are SURVEY.md
+Roofline: the dominant stage is the intersect stage (the reference's pathTraceOneBounce*): k_geoms
+(the analytic geoms and the KD root-box test; rays that miss the root box end there) then k_trace (the
+KD traversal of the rest).  HBM-bound; algorithmic bytes per segment are SURVEY.md
 8(d)'s B = 352 + 52*N_aabb + 36*N_tri + 40*N_hit restricted to the intersect kernel:
 B_trace = 76 + 52*N_aabb + 36*N_tri + 40*N_hit (PathSegment read 56 + ShadeableIntersection
 write 20, plus the tree/triangle bytes), with N_* from an untimed counting iteration; achieved =
-B_trace x segments per launch / the average launch time during the timed steps, measured on the
-device clock inside the kernel (first workgroup start to last workgroup end; agrees with rocprofv3's
-kernel-trace durations).  HIP events on the launching stream are reported beside it: with several
+B_trace x segments per launch / the average stage time per bounce launch during the timed steps, measured
+on the device clock inside the kernels (first workgroup start to last workgroup end of k_geoms, plus
+the same for k_trace; agrees with rocprofv3's kernel-trace durations).  HIP events on the launching stream are reported beside it: with several
 iterations in flight they also count the time a launch waits behind the other iterations' kernels.
 """
 from __future__ import annotations
@@ -45,8 +46,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=32)
+    ap.add_argument("--warmup", type=int, default=4)
     ap.add_argument("--mesh", default="dragon_5")
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--res", type=int, nargs=2, default=(800, 800))
@@ -56,9 +57,9 @@ def parse():
                     help="bounces per iteration (8 = the reference's `depth > 7`; 16 for the C5 stress config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--pipeline", type=int, default=2,
+    ap.add_argument("--pipeline", type=int, default=3,
                     help="batches in flight (kdpt_trace_iterations; bit-identical to one at a time)")
-    ap.add_argument("--batch", type=int, default=2, help="iterations sharing each intersect launch (<= 4)")
+    ap.add_argument("--batch", type=int, default=4, help="iterations sharing each intersect launch (<= 4)")
     return ap.parse_args()
 
 
@@ -191,7 +192,8 @@ def main():
         "primary_rays_per_s": round(W * H * args.steps * world / dt, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_trace (intersect: analytic geoms + KD traversal)",
+                     "kernel": "intersect stage = k_geoms (analytic geoms + KD root-box test, candidate list) "
+                               "+ k_trace (KD traversal of the candidates)",
                      "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
                      "avg_launch_ms_events": round(ev_ms / max(1, ev_launches), 5),
                      "aggregate_GBps": round(per_seg_bytes * seg / dt / 1e9, 2),
@@ -200,10 +202,10 @@ def main():
                                             "hit": round(hit / count_seg, 5)}},
         "reference_980m_intersect_ms_per_iter": 79.4,
         "intersect_ms_per_iter": round(kernel_ms / (args.steps * world), 4),
-        "timing_note": "avg_launch_ms: intersect launches on the device clock (s_memrealtime, first block start to "
-                       "last block end), comparable with rocprofv3 kernel-trace durations; avg_launch_ms_events: HIP "
-                       "events on the launching stream, which also count queueing behind the other in-flight "
-                       "iterations' kernels",
+        "timing_note": "avg_launch_ms: intersect stage per bounce launch on the device clock (s_memrealtime, first "
+                       "block start to last block end of k_geoms plus the same of k_trace), comparable with "
+                       "rocprofv3 kernel-trace durations; avg_launch_ms_events: HIP events on the launching stream "
+                       "around both, which also count queueing behind the other in-flight iterations' kernels",
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)

@@ -91,7 +91,8 @@ struct DevScene {
   int n0_left, n0_right, n1_left, n1_right;
   // big leaves (>= BIG_LEAF triangles) as clusters of <= 64 triangles in Morton order, each with its
   // box: leaf_cl[node] = {first cluster, count} (count 0: not big); cl_lo/cl_hi boxes; cl_info =
-  // {first triangle, size}; cluster-order copies of v0/e1/e2 with the original index in e1.w
+  // {first triangle, size}; cluster-order copies of v0/e1/e2 with the original index in e1.w, each
+  // cluster padded to 64 entries (cluster c = entries [64c, 64c + 64); padding: zeros, index -1)
   const int2* leaf_cl;
   int num_clusters;
   const float4* cl_lo;
@@ -480,6 +481,10 @@ __device__ inline void prof_lap(WaveLeafLDS* W, int k) {  // cycles since the la
 
 constexpr int BIG_LEAF = 64;  // leaves this size or larger are swept by the whole wave, one at a time
 
+__device__ inline float readlane_f(float v, int lane) {
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+
 __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
 #pragma unroll
   for (int off = 32; off > 0; off >>= 1) {
@@ -732,12 +737,13 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     // Recombination by ORIGINAL index: last u/v pass = max index, last hit = max, best = min (t, index).
     const int j = __builtin_ctzll(bigmask);
     bigmask &= bigmask - 1;
-    const int jfirst = __builtin_amdgcn_readfirstlane(
-        NodeSrc::kLeafHoldsCluster ? __shfl(lstart, j) : S.leaf_cl[__shfl(lnode, j)].x);
-    const int jcount = (__builtin_amdgcn_readfirstlane(__shfl(lsize, j)) + 63) >> 6;
-    const f3 jo = mk3(__shfl(o.x, j), __shfl(o.y, j), __shfl(o.z, j));
-    const f3 jd = mk3(__shfl(d.x, j), __shfl(d.y, j), __shfl(d.z, j));
-    const f3 jinv = mk3(__shfl(invdir.x, j), __shfl(invdir.y, j), __shfl(invdir.z, j));
+    const int jfirst = NodeSrc::kLeafHoldsCluster ? __builtin_amdgcn_readlane(lstart, j)
+                                                  : S.leaf_cl[__builtin_amdgcn_readlane(lnode, j)].x;
+    const int jcount = (__builtin_amdgcn_readlane(lsize, j) + 63) >> 6;
+    // lane j's ray, wave-uniform: read into scalar registers
+    const f3 jo = mk3(readlane_f(o.x, j), readlane_f(o.y, j), readlane_f(o.z, j));
+    const f3 jd = mk3(readlane_f(d.x, j), readlane_f(d.y, j), readlane_f(d.z, j));
+    const f3 jinv = mk3(readlane_f(invdir.x, j), readlane_f(invdir.y, j), readlane_f(invdir.z, j));
     const int2 cr = make_int2(jfirst, jcount);
     unsigned long long u_pass = 0ull, u_best = ~0ull;
     int u_lasthit = -1, u_nhit = 0;
@@ -748,17 +754,29 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
      const int cq = cv ? ck : cr.x;
      unsigned long long cmask =
          __ballot(cv && (!fastAABB || cluster_may_pass(clusters.lo_of(cq), clusters.hi_of(cq), jo, jinv)));
-     while (cmask) {
-      const int c = cr.x + cb0 + __builtin_ctzll(cmask);
-      cmask &= cmask - 1;
+     // clusters are padded to 64 entries (padding never passes: e1 = e2 = 0), so cluster c's triangles
+     // are c*64 + lane; the next surviving cluster's triangles are fetched while this one is tested
+     int c = -1;
+     TriData T{};
+     if (cmask) {
+       c = cr.x + cb0 + __builtin_ctzll(cmask);
+       cmask &= cmask - 1;
+       const int ct = c * 64 + lane;
+       T = TriData{S.c_v0[ct], S.c_e1[ct], S.c_e2[ct]};
+     }
+     while (c >= 0) {
+      int cn = -1;
+      TriData Tn{};
+      if (cmask) {
+        cn = cr.x + cb0 + __builtin_ctzll(cmask);
+        cmask &= cmask - 1;
+        const int ctn = cn * 64 + lane;
+        Tn = TriData{S.c_v0[ctn], S.c_e1[ctn], S.c_e2[ctn]};
+      }
       if (COUNT) prof_add(W, PROF_BIG_SWEEPS, 1);
-      const int2 ci = S.cl_info[c];
-      const bool in = lane < ci.y;
-      const int ct = ci.x + (in ? lane : 0);
-      const TriData T{S.c_v0[ct], S.c_e1[ct], S.c_e2[ct]};
       const int orig = fbits(T.e1.w);
       float bx = 0, by = 0, bzk = 0;
-      const int r = in ? tri_test_v(T, jo, jd, bx, by, bzk) : 0;
+      const int r = tri_test_v(T, jo, jd, bx, by, bzk);
       if (__ballot(r >= 1)) {
         const unsigned long long pk =
             r >= 1 ? ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk) : 0ull;
@@ -778,6 +796,8 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
           u_best = wb < u_best ? wb : u_best;
         }
       }
+      c = cn;
+      T = Tn;
      }
     }
     if (lane == j) {

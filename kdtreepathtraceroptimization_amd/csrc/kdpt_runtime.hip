@@ -82,8 +82,11 @@ __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int
     for (int k = 1; k < ncounts; k++) counts[k] = 0;
     for (int k = 0; k < nwork; k++) {
       work[k] = 0;
-      trace_t[2 * k] = ~0ull;
+      work[nwork + k] = 0;  // candidate counts (k_geoms), stored after the work counters
+      trace_t[2 * k] = ~0ull;  // k_trace span of bounce k, then (at 2*nwork) k_geoms' span
       trace_t[2 * k + 1] = 0ull;
+      trace_t[2 * nwork + 2 * k] = ~0ull;
+      trace_t[2 * nwork + 2 * k + 1] = 0ull;
     }
   }
   if (index >= W * H) return;
@@ -147,10 +150,10 @@ constexpr int TRACE_BLOCK = 1024;
 constexpr int MAXB = 4;
 struct TraceIter {
   PathBuf paths;
-  const int* perm;      // trace order (queue slot -> path index), or null for identity
+  const int* cand;      // k_geoms' list of the paths whose ray meets the KD root box (queue slot -> path)
+  const int* ccount;    // ... and its length per bounce
   const int2* geomhit;  // k_geoms' {t_min bits, geom index} per path
   int2* hits;
-  const int* counts;
 };
 
 struct TraceArgs {
@@ -160,7 +163,8 @@ struct TraceArgs {
   int* work;  // chunk counters, zeroed by k_gen_rays (of iteration 0 of the batch)
   int depth;
   Counters* counters;
-  unsigned long long* trace_t;  // [2 * cap] first block start / last block end (s_memrealtime)
+  unsigned long long* trace_t;  // [4 * cap]: per bounce first block start / last block end (s_memrealtime)
+                                // of k_trace, then of k_geoms (at 2 * cap)
 };
 
 __device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, WaveLeafLDS* W,
@@ -186,40 +190,82 @@ __device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, 
 
 // The analytic geoms of pathTraceOneBounceKDbare (tested before the KD tree; src/pathtrace.cu:1600-1640),
 // one lane per live path, consecutive paths per wave: {t_min bits, geom index} for k_trace.
-__global__ __launch_bounds__(256) void k_geoms(DevScene S, PathBuf paths, const int* counts, int depth,
-                                               int2* __restrict__ geomhit) {
+//
+// The KD traversal's first step tests the root's box, and a ray that misses it ends there with no other
+// effect (traverseKDbareShortHybrid: `!hitGeom && parentID == -1` -> break), so such a ray's hit record
+// is final here: it is written now, and only the rays that meet the root box are listed (cand, ccount)
+// for the intersect kernel -- whose lanes then all hold rays that actually walk the tree.
+constexpr int GEOM_BLOCK = 1024;  // k_geoms: one candidate-list atomic per 1024 paths
+__global__ __launch_bounds__(GEOM_BLOCK) void k_geoms(DevScene S, PathBuf paths, const int* counts, int depth,
+                                               int2* __restrict__ geomhit, int2* __restrict__ hits,
+                                               int* __restrict__ cand, int* __restrict__ ccount,
+                                               Counters* count_aabb, unsigned long long* gspan) {
   const int n = counts[depth];
+  if ((int)(blockIdx.x * blockDim.x) >= n) return;  // uniform per block
+  if (threadIdx.x == 0) atomicMin(&gspan[2 * depth], (unsigned long long)__builtin_amdgcn_s_memrealtime());
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i >= n) return;
-  const float4 q1 = paths.p1[i];
-  if (fbits(paths.p2[i].w) <= 0) return;
-  const float4 q0 = paths.p0[i];
-  Ray ray;
-  ray.origin = mk3(q0.x, q0.y, q0.z);
-  ray.direction = mk3(q1.x, q1.y, q1.z);
-  ray.isinside = false;
-  ray.sdepth = q0.w;
-  float t_min = FLT_MAXV;
-  int hit = -1;
-  f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
-  float t = 0;
-  const f3 inv = mk3(1.0f / ray.direction.x, 1.0f / ray.direction.y, 1.0f / ray.direction.z);
-  const bool finite = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
-  for (int g = 0; g < S.num_geoms; g++) {
-    const DevGeom& G = S.geoms[g];
-    if (finite && !geom_may_hit(G, ray.origin, inv)) {
-      t = -1.0f;  // the exact test would miss
-    } else if (G.type == 1) {
-      t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
-    } else if (G.type == 0) {
-      t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+  const bool kd = S.has_obj && S.num_nodes > 0;
+  bool tested = false, walk = false;  // traversed at all / goes on to the intersect kernel
+  // finished paths (compaction off) are skipped, as pathTraceOneBounce* skips them
+  if (i < n && fbits(paths.p2[i].w) > 0) {
+    const float4 q0 = paths.p0[i], q1 = paths.p1[i];
+    Ray ray;
+    ray.origin = mk3(q0.x, q0.y, q0.z);
+    ray.direction = mk3(q1.x, q1.y, q1.z);
+    ray.isinside = false;
+    ray.sdepth = q0.w;
+    float t_min = FLT_MAXV;
+    int hit = -1;
+    f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
+    float t = 0;
+    const f3 inv = mk3(1.0f / ray.direction.x, 1.0f / ray.direction.y, 1.0f / ray.direction.z);
+    const bool finite = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
+    for (int g = 0; g < S.num_geoms; g++) {
+      const DevGeom& G = S.geoms[g];
+      if (finite && !geom_may_hit(G, ray.origin, inv)) {
+        t = -1.0f;  // the exact test would miss
+      } else if (G.type == 1) {
+        t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
+      } else if (G.type == 0) {
+        t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+      }
+      if (t > 0.0f && t_min > t) {
+        t_min = t;
+        hit = g;
+      }
     }
-    if (t > 0.0f && t_min > t) {
-      t_min = t;
-      hit = g;
+    if (kd) {  // the traversal's first step: the root's box (same intersectAABB, same invdir)
+      float dist;
+      tested = true;
+      walk = intersectAABB(ray.origin, inv, make_float4(S.rlo.x, S.rlo.y, S.rlo.z, S.rhi.x),
+                           make_float4(S.rhi.y, S.rhi.z, 0.0f, 0.0f), dist);
     }
+    if (walk) geomhit[i] = make_int2(fbits(t_min), hit);
+    else hits[i] = make_int2(hit, -1);  // final: the analytic geoms' hit (code -1: none)
   }
-  geomhit[i] = make_int2(fbits(t_min), hit);
+  // append the walking rays to the candidate list: one atomic per block (a single counter hit once
+  // per wave by ~10k waves serialises for ~100 us at 800x800)
+  __shared__ int s_wcount[GEOM_BLOCK / 64], s_base;
+  const unsigned long long wm = __ballot(walk);
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  if (lane == 0) s_wcount[wv] = __popcll(wm);
+  if (count_aabb) {  // count mode: the root test of the rays that end here
+    const unsigned long long miss = __ballot(tested && !walk);
+    if (lane == 0 && miss) atomicAdd(&count_aabb->aabb, (unsigned long long)__popcll(miss));
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int tot = 0;
+    for (int w = 0; w < GEOM_BLOCK / 64; w++) {
+      const int c = s_wcount[w];
+      s_wcount[w] = tot;
+      tot += c;
+    }
+    s_base = tot ? atomicAdd(&ccount[depth], tot) : 0;
+  }
+  __syncthreads();
+  if (walk) cand[s_base + s_wcount[wv] + (int)lane_prefix(wm)] = i;
+  if (threadIdx.x == 0) atomicMax(&gspan[2 * depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
 // KD traversal of every live path.  Each lane holds one ray; whenever rays finish, the idle lanes take
@@ -233,7 +279,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
   int pre[MAXB + 1];  // the batch's paths, concatenated: iteration b owns queue slots [pre[b], pre[b+1])
   pre[0] = 0;
 #pragma unroll
-  for (int b = 0; b < MAXB; b++) pre[b + 1] = pre[b] + (b < A.nb ? A.it[b].counts[A.depth] : 0);
+  for (int b = 0; b < MAXB; b++) pre[b + 1] = pre[b] + (b < A.nb ? A.it[b].ccount[A.depth] : 0);
   const int n = pre[MAXB];
   if (MODE == TREE_LDS) {
     if (n == 0) return;  // uniform: nothing to trace
@@ -266,12 +312,14 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
   R.done = true;
   int pidx = -1;  // the lane's path (-1: idle)
   int pb = 0;     // ... and the batch iteration it belongs to
-  // The first 64 paths of each wave are its own (no atomic: thousands of waves start at once); the
-  // counter hands out the rest, starting after them.
+  // Path slots: each wave first takes a static run of ceil(n / nwaves) (at most 64) consecutive slots,
+  // so that every CU gets work even when a bounce has few rays (the kernel is issue-bound: rays piled
+  // onto a few CUs would leave the others idle); a device counter hands out the rest, exactly as many
+  // as the wave has idle lanes, so the tail of the bounce stays balanced.
   const int nwaves = gridDim.x * (TRACE_BLOCK / 64);
   const int wid = blockIdx.x * (TRACE_BLOCK / 64) + (threadIdx.x >> 6);
+  const int srun = min(64, max(1, (n + nwaves - 1) / nwaves));
   bool first = true, exhausted = false;
-  const bool kd = S.has_obj && S.num_nodes > 0;
   long long rounds = 0;
   while (true) {
     if (__ballot(1) != ~0ull) {  // the refill protocol needs the whole wave here
@@ -279,43 +327,35 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
       break;
     }
     // ---- refill idle lanes ----
-    if (!exhausted) {
-      if (COUNT) prof_lap(W, -1);
-      const unsigned long long im = __ballot(pidx < 0);
-      if (im) {
-        int base;
-        bool last;
-        if (first) {  // static round: slots [wid*64, wid*64 + 64)
-          base = wid * 64;
-          first = false;
-          last = nwaves * 64 >= n;
-        } else {
-          int b = 0;
-          if (lane == 0) b = nwaves * 64 + atomicAdd(work, __popcll(im));
-          base = __shfl(b, 0);
-          last = base + __popcll(im) >= n;  // the counter only grows: later rounds find nothing
-        }
-        if (pidx < 0) {
-          const int k = base + (int)lane_prefix(im);
-          if (k < n) {
-            const int b = (k >= pre[1]) + (k >= pre[2]) + (k >= pre[3]);
-            const TraceIter& I = b == 0 ? A.it[0] : (b == 1 ? A.it[1] : (b == 2 ? A.it[2] : A.it[3]));
-            const int local = k - (b == 0 ? 0 : (b == 1 ? pre[1] : (b == 2 ? pre[2] : pre[3])));
-            const int i = I.perm ? I.perm[local] : local;
-            const float4 q0 = I.paths.p0[i], q1 = I.paths.p1[i];
-            if (fbits(I.paths.p2[i].w) > 0) {  // no work for finished paths (compaction off)
-              const int2 gh = I.geomhit[i];
-              pidx = i;
-              pb = b;
-              wave_ray_start(S, R, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z), u2f((uint32_t)gh.x), gh.y, W);
-              if (!kd) R.done = true;
-            }
-          }
-        }
-        exhausted = last;
+    if (COUNT) prof_lap(W, -1);
+    const unsigned long long im = exhausted ? 0ull : __ballot(pidx < 0);
+    if (im) {
+      const int p = (int)lane_prefix(im);
+      int k;
+      if (first) {  // static run: slots [wid*srun, wid*srun + srun)
+        first = false;
+        k = p < srun ? wid * srun + p : n;
+        exhausted = (long long)nwaves * srun >= n;
+      } else {
+        int b = 0;
+        if (lane == 0) b = nwaves * srun + atomicAdd(work, __popcll(im));
+        const int base = __shfl(b, 0);
+        k = base + p;
+        exhausted = base + __popcll(im) >= n;  // the counter only grows: later rounds find nothing
       }
-      if (COUNT) prof_lap(W, PROF_SETUP_CYC);
+      if (pidx < 0 && k < n) {
+        const int b = (k >= pre[1]) + (k >= pre[2]) + (k >= pre[3]);
+        const TraceIter& I = b == 0 ? A.it[0] : (b == 1 ? A.it[1] : (b == 2 ? A.it[2] : A.it[3]));
+        const int local = k - (b == 0 ? 0 : (b == 1 ? pre[1] : (b == 2 ? pre[2] : pre[3])));
+        const int i = I.cand[local];
+        const float4 q0 = I.paths.p0[i], q1 = I.paths.p1[i];
+        const int2 gh = I.geomhit[i];
+        pidx = i;
+        pb = b;
+        wave_ray_start(S, R, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z), u2f((uint32_t)gh.x), gh.y, W);
+      }
     }
+    if (COUNT) prof_lap(W, PROF_SETUP_CYC);
     const bool busy = pidx >= 0 && !R.done;
     if (__any(busy)) {
       const bool fastAABB = __all(!busy || (fabsf(R.invdir.x) < FLT_INFV && fabsf(R.invdir.y) < FLT_INFV &&
@@ -554,6 +594,7 @@ struct ShadeArgs {
   int nkeys;
   unsigned long long* total_segments;  // running sum of paths launched into the intersect kernel
   const unsigned long long* trace_t;   // this bounce's intersect launch record (see TraceArgs)
+  const unsigned long long* gspan;     // ... and the k_geoms launches' record
   unsigned long long* trace_total;     // [2]: summed launch ticks, launches
 };
 
@@ -565,9 +606,13 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   const int i = tile * TILE + threadIdx.x;
   if (i == 0) {
     atomicAdd(A.total_segments, (unsigned long long)n);
+    // the intersect stage of this bounce on the device clock: k_geoms' span + k_trace's span (a kernel
+    // that had nothing to do left its record empty)
     const unsigned long long t0 = A.trace_t[2 * A.depth], t1 = A.trace_t[2 * A.depth + 1];
-    if (A.trace_total && t1 > t0) {  // the intersect launch before this one on the stream ran (n > 0)
-      atomicAdd(&A.trace_total[0], t1 - t0);
+    const unsigned long long g0 = A.gspan[2 * A.depth], g1 = A.gspan[2 * A.depth + 1];
+    const unsigned long long span = (t1 > t0 ? t1 - t0 : 0ull) + (g1 > g0 ? g1 - g0 : 0ull);
+    if (A.trace_total && span) {
+      atomicAdd(&A.trace_total[0], span);
       atomicAdd(&A.trace_total[1], 1ull);
     }
   }
@@ -873,6 +918,8 @@ struct kdpt_ctx {
   int* work = nullptr;
   int2* hits = nullptr;   // [npix] hit code + objMaterialIdx from the intersect kernel
   int2* geomhit = nullptr;  // [npix] analytic-geom t_min bits + index (k_geoms -> k_trace)
+  int* cand = nullptr;      // [npix] paths whose ray meets the KD root box (k_geoms -> k_trace)
+  int* ccount = nullptr;    // [cap] their number per bounce (inside the counts allocation)
   int tree_mode = 0;      // TreeMode
   int trace_grid = 0;     // persistent intersect workgroups
   size_t tree_lds = 0;    // dynamic LDS bytes of the intersect kernel (TREE_LDS)
@@ -969,9 +1016,10 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
   }
   // counts[0..cap+1]: live paths per bounce (rewritten every iteration); counts[cap+2]: fault flag;
   // counts[cap+3 ..]: work counters of the persistent intersect kernel
-  if ((rc = dalloc(c, &c->trace_t, 2 * (size_t)c->cap))) return rc;
-  HIP_TRY(hipMemset(c->trace_t, 0, sizeof(unsigned long long) * 2 * c->cap));
-  if ((rc = dalloc(c, &c->counts, 2 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
+  if ((rc = dalloc(c, &c->trace_t, 4 * (size_t)c->cap))) return rc;
+  HIP_TRY(hipMemset(c->trace_t, 0, sizeof(unsigned long long) * 4 * c->cap));
+  if ((rc = dalloc(c, &c->counts, 3 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
+      (rc = dalloc(c, &c->cand, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->geomhit, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->perm, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->tile_kcounts, (size_t)TRACE_KEYS * c->ntiles)) ||
@@ -981,9 +1029,10 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
     return rc;
   if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 3), hipHostMallocDefault) != hipSuccess)
     return fail(KDPT_ERR_HIP, "hipHostMalloc");
-  HIP_TRY(hipMemset(c->counts, 0, sizeof(int) * (2 * c->cap + 3)));
+  HIP_TRY(hipMemset(c->counts, 0, sizeof(int) * (3 * c->cap + 3)));
   c->S.fault = c->counts + c->cap + 2;
   c->work = c->counts + c->cap + 3;
+  c->ccount = c->work + c->cap;
   return KDPT_OK;
 }
 
@@ -1113,6 +1162,11 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
         q.w = ibits(t);  // original triangle index
         ce1.push_back(q);
         ce2.push_back(e2[t]);
+      }
+      for (int k = cnt; k < 64; k++) {  // padding: e1 = e2 = 0 fails glm's determinant test
+        cv0.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        ce1.push_back(make_float4(0.0f, 0.0f, 0.0f, ibits(-1)));
+        ce2.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
       }
       lo.push_back(make_float4(l[0], l[1], l[2], 0.0f));
       hi.push_back(make_float4(h[0], h[1], h[2], 0.0f));
@@ -1256,7 +1310,7 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   if (o.bounce_cap > 30) return fail(KDPT_ERR_ARG, "bounce_cap > 30");
   if (o.block_size && o.block_size != TILE) return fail(KDPT_ERR_UNSUPPORTED, "block_size must be 0 or 256");
   const int W = sc->camera.resolution[0], H = sc->camera.resolution[1];
-  if (W <= 0 || H <= 0 || (long long)W * H > (1ll << 30)) return fail(KDPT_ERR_ARG, "bad resolution");
+  if (W <= 0 || H <= 0 || (long long)W * H >= (1ll << 30)) return fail(KDPT_ERR_ARG, "bad resolution");
   if (sc->num_materials > MAX_KEYS) return fail(KDPT_ERR_UNSUPPORTED, "more than 64 materials");
   // The compact visited-state traversal needs the reference builder's shape:
   // nodes[i].ID == i, root == node 0, node 1 == root's left child, <= 15 levels.
@@ -1524,7 +1578,7 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     const char* cw = getenv("KDPT_CHUNK_WIDTHS");  // e.g. "16,32,64"
     if (cw) sscanf(cw, "%d,%d,%d", &c->chunk_width[0], &c->chunk_width[1], &c->chunk_width[2]);
     for (int k = 0; k < 3; k++) c->chunk_width[k] = std::min(64, std::max(1, c->chunk_width[k]));
-    c->trace_order = c->S.trace_mode > 0 && c->S.has_obj && c->S.num_nodes > 0;
+    c->trace_order = false;  // superseded by k_geoms' candidate lists (KDPT_TRACE_ORDER is ignored)
   }
   if ((rc = setup_trace(c))) return bail(rc);
   c->S.trip_limit = 8 * std::max(c->S.num_nodes, 1) + 64;
@@ -1980,10 +2034,10 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     for (int b = 0; b < MAXB; b++) {
       kdpt_ctx* c = cs[b < nb ? b : 0];
       t.it[b].paths = c->buf[c->cur];
-      t.it[b].perm = (depth > 0 && compact && c->trace_order) ? c->perm : nullptr;
+      t.it[b].cand = c->cand;
+      t.it[b].ccount = c->ccount;
       t.it[b].geomhit = c->geomhit;
       t.it[b].hits = c->hits;
-      t.it[b].counts = c->counts;
     }
     t.work = c0->work;
     t.depth = depth;
@@ -2022,8 +2076,10 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     } else {
       for (int b = 0; b < nb; b++) {
         kdpt_ctx* c = cs[b];
-        hipLaunchKernelGGL(k_geoms, dim3(c->ntiles), dim3(TILE), 0, st, c->S, c->buf[c->cur], c->counts, depth,
-                           c->geomhit);
+        hipLaunchKernelGGL(k_geoms, dim3((c->npix + GEOM_BLOCK - 1) / GEOM_BLOCK), dim3(GEOM_BLOCK), 0, st, c->S,
+                           c->buf[c->cur], c->counts, depth,
+                           c->geomhit, c->hits, c->cand, c->ccount, count ? c0->counters : nullptr,
+                           c0->trace_t + 2 * c0->cap);
         HIP_TRY(hipGetLastError());
       }
       launch_trace(c0, t, count, st);
@@ -2055,6 +2111,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       a.nkeys = c->nkeys;
       a.total_segments = c->total_segments;
       a.trace_t = c0->trace_t;
+      a.gspan = c0->trace_t + 2 * c0->cap;
       a.trace_total = b == 0 ? c->trace_total : nullptr;
       // hit point offset: 1e-4 for the hybrid traversal and the brute-force kernel, 1e-5 for traverseKDbare
       if (c->opt.short_stack || c->brute) launch_shade_h<true>(c, a, compact, sort, st);
