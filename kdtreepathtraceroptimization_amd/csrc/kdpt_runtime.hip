@@ -143,7 +143,11 @@ __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int
 // same functions, so nothing else needs to travel.
 // ---------------------------------------------------------------------------
 enum TreeMode { TREE_WIDE = 0, TREE_PACKED = 1, TREE_LDS = 2 };
-constexpr int TRACE_BLOCK = 1024;
+constexpr int TRACE_BLOCK = 1024;  // LDS mode: one workgroup per CU shares the tree copy
+// workgroup size of the intersect kernel: with the tree in LDS every wave of a CU must share the copy,
+// otherwise small workgroups let the tail of one launch hold only a quarter of a CU
+template <int MODE>
+constexpr int trace_block() { return MODE == 2 ? TRACE_BLOCK : 256; }
 
 // Up to MAXB iterations (each its own path buffers) at the same bounce share one intersect launch:
 // more rays per launch keep the lanes of the persistent waves busy.
@@ -272,9 +276,10 @@ __global__ __launch_bounds__(GEOM_BLOCK) void k_geoms(DevScene S, PathBuf paths,
 // the next paths of the bounce from a device counter, so a wave stays full until the bounce runs out
 // of paths (the per-ray algorithm is unchanged -- only which lane runs it, and when).
 template <bool HYBRID, bool COUNT, int MODE>
-__global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
+__global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
+  constexpr int TB = trace_block<MODE>();
   extern __shared__ int4 s_tree[];
-  __shared__ WaveLeafLDS s_leaf[TRACE_BLOCK / 64];
+  __shared__ WaveLeafLDS s_leaf[TB / 64];
   const DevScene& S = A.S;
   int pre[MAXB + 1];  // the batch's paths, concatenated: iteration b owns queue slots [pre[b], pre[b+1])
   pre[0] = 0;
@@ -284,9 +289,9 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
   if (MODE == TREE_LDS) {
     if (n == 0) return;  // uniform: nothing to trace
     const int words = 2 * S.num_nodes;
-    for (int k = threadIdx.x; k < words; k += TRACE_BLOCK) s_tree[k] = S.pnodes[k];
+    for (int k = threadIdx.x; k < words; k += TB) s_tree[k] = S.pnodes[k];
     float4* s_cl = reinterpret_cast<float4*>(s_tree + words);
-    for (int k = threadIdx.x; k < S.num_clusters; k += TRACE_BLOCK) {
+    for (int k = threadIdx.x; k < S.num_clusters; k += TB) {
       s_cl[2 * k] = S.cl_lo[k];
       s_cl[2 * k + 1] = S.cl_hi[k];
     }
@@ -316,8 +321,8 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
   // so that every CU gets work even when a bounce has few rays (the kernel is issue-bound: rays piled
   // onto a few CUs would leave the others idle); a device counter hands out the rest, exactly as many
   // as the wave has idle lanes, so the tail of the bounce stays balanced.
-  const int nwaves = gridDim.x * (TRACE_BLOCK / 64);
-  const int wid = blockIdx.x * (TRACE_BLOCK / 64) + (threadIdx.x >> 6);
+  const int nwaves = gridDim.x * (TB / 64);
+  const int wid = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
   const int srun = min(64, max(1, (n + nwaves - 1) / nwaves));
   bool first = true, exhausted = false;
   long long rounds = 0;
@@ -393,7 +398,7 @@ __global__ __launch_bounds__(TRACE_BLOCK) void k_trace(TraceArgs A) {
       atomicAdd(&A.counters->life[us10 < 63 ? us10 : 63], 1ull);
     }
   }
-  if (lane == 0 && atomicAdd(&s_waves_done, 1) == TRACE_BLOCK / 64 - 1)
+  if (lane == 0 && atomicAdd(&s_waves_done, 1) == TB / 64 - 1)
     atomicMax(&A.trace_t[2 * A.depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
@@ -1217,7 +1222,7 @@ int trace_occupancy(kdpt_ctx* c, size_t lds, int* blocks) {
   if (lds > 0)
     HIP_TRY(hipFuncSetAttribute((const void*)k_trace<HYBRID, COUNT, MODE>,
                                 hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace<HYBRID, COUNT, MODE>, TRACE_BLOCK, lds));
+  HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(blocks, k_trace<HYBRID, COUNT, MODE>, trace_block<MODE>(), lds));
   return KDPT_OK;
 }
 
@@ -1230,7 +1235,9 @@ int setup_trace(kdpt_ctx* c) {
   const size_t static_lds = sizeof(WaveLeafLDS) * (TRACE_BLOCK / 64);
   const size_t tree_bytes = 32 * (size_t)c->S.num_nodes + 32 * (size_t)c->S.num_clusters;  // + cluster boxes
   const size_t lds_max = prop.sharedMemPerBlock > 0 ? prop.sharedMemPerBlock : 65536;
-  if (c->S.pnodes && static_lds + tree_bytes <= lds_max) {
+  const char* tm = getenv("KDPT_TREE");  // "global": keep the tree in HBM/L2 (experiments)
+  const bool force_global = tm && strcmp(tm, "global") == 0;
+  if (c->S.pnodes && static_lds + tree_bytes <= lds_max && !force_global) {
     c->tree_mode = TREE_LDS;
     c->tree_lds = tree_bytes;
   }
@@ -1983,7 +1990,7 @@ namespace {
 
 template <bool HYBRID, bool COUNT>
 void launch_trace_mode(kdpt_ctx* c, const TraceArgs& a, hipStream_t st) {
-  const dim3 g(c->trace_grid), b(TRACE_BLOCK);
+  const dim3 g(c->trace_grid), b(c->tree_mode == TREE_LDS ? trace_block<TREE_LDS>() : trace_block<TREE_PACKED>());
   if (c->tree_mode == TREE_LDS)
     hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS>), g, b, c->tree_lds, st, a);
   else if (c->tree_mode == TREE_PACKED)
