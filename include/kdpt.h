@@ -152,7 +152,7 @@ typedef struct kdpt_options {
     int testing_mode;    /* 0: 1 = also time the intersect kernel per bounce (TESTINGMODE) */
     int compaction;      /* 1 */
     int enable_kd;       /* 1; 0 = brute force over the OBJ arrays (pathTraceOneBounce) */
-    int viz_kd;          /* 0 (box visualisation, not built) */
+    int viz_kd;          /* 0; 1 = KD node boxes drawn as boxes (pathTraceOneBounceKDbareBoxes) */
     int use_bbox;        /* 0; brute force only: each shape's bbox test first (src/pathtrace.cu:497-513) */
     int short_stack;     /* 1: traverseKDbareShortHybrid, 0: traverseKDbare */
     int bounce_cap;      /* 8 == `depth > 7` (src/pathtrace.cu:2608); 16 for the stress config */

@@ -69,6 +69,7 @@ KDPT_HD bool geom_may_hit(const DevGeom& G, f3 o, f3 invdir) {
 struct DevScene {
   const DevGeom* geoms;
   int num_geoms;
+  int num_boxes;  // viz_kd: the KD node boxes, stored after the analytic geoms in `geoms`
   const DevMaterial* materials;
   int num_materials;
   int has_obj;

@@ -27,6 +27,10 @@
 
 using namespace kdpt;
 
+namespace kdpt_host {
+void node_box_matrices(const float* mins, const float* maxs, float* transform16, float* inverse16);
+}
+
 namespace {
 
 constexpr int TILE = 256;  // paths per workgroup (4 waves of 64)
@@ -579,6 +583,48 @@ __global__ __launch_bounds__(TILE) void k_brute(BruteArgs A) {
 }
 
 // ---------------------------------------------------------------------------
+// pathTraceOneBounceKDbareBoxes (src/pathtrace.cu:1738-1885, viz_kd): the analytic geoms, then every KD
+// node's box as a box (boxIntersectionTestBox = boxIntersectionTest of the node's unit-cube transform).
+// One lane per path; the node index is wave-uniform, so each box's matrices are scalar loads.  A winning
+// node box k is reported as geom num_geoms + k (its record carries material num_materials - 1), which
+// k_shade recomputes like any analytic geom.
+// ---------------------------------------------------------------------------
+__global__ __launch_bounds__(TILE) void k_viz(DevScene S, PathBuf paths, const int* counts, int depth, int2* hits,
+                                               unsigned long long* trace_t) {
+  const int n = counts[depth];
+  if ((int)blockIdx.x * TILE >= n) return;
+  if (threadIdx.x == 0) atomicMin(&trace_t[2 * depth], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  const int i = blockIdx.x * TILE + threadIdx.x;
+  if (i < n && fbits(paths.p2[i].w) > 0) {
+    const float4 q0 = paths.p0[i], q1 = paths.p1[i];
+    Ray ray;
+    ray.origin = mk3(q0.x, q0.y, q0.z);
+    ray.direction = mk3(q1.x, q1.y, q1.z);
+    ray.isinside = false;
+    ray.sdepth = q0.w;
+    const f3 inv = mk3(1.0f / ray.direction.x, 1.0f / ray.direction.y, 1.0f / ray.direction.z);
+    const bool finite = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
+    float t_min = FLT_MAXV, t = 0;
+    int hit = -1;
+    f3 tmp_i, tmp_n;
+    const int total = S.num_geoms + (S.has_obj ? S.num_boxes : 0);
+    for (int g = 0; g < total; g++) {
+      const DevGeom& G = S.geoms[g];
+      if (finite && !geom_may_hit(G, ray.origin, inv)) t = -1.0f;
+      else if (G.type == 1) t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
+      else if (G.type == 0) t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+      if (t > 0.0f && t_min > t) {
+        t_min = t;
+        hit = g;
+      }
+    }
+    hits[i] = make_int2(hit, -1);
+  }
+  __syncthreads();
+  if (threadIdx.x == 0) atomicMax(&trace_t[2 * depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
+// ---------------------------------------------------------------------------
 // shadeMaterial + scatterRay (src/pathtrace.cu:1885-2100, src/interactions.h) +
 // partialGather, one lane per live path; writes the path in place and the tile's
 // survivor count (or, when sorting, its per-material histogram).
@@ -964,6 +1010,7 @@ struct kdpt_ctx {
   long long intersect_launches_total = 0;
   // enable_kd = 0: brute-force intersect kernel over the OBJ triangles in file order
   bool brute = false;
+  bool viz = false;  // viz_kd: the KD node boxes drawn as boxes (k_viz)
   BruteShape* shapes = nullptr;
   int num_shapes = 0;
 };
@@ -1077,6 +1124,7 @@ int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
   c->wall_khz = p->wall_khz;
   c->sync_debug = p->sync_debug;
   c->brute = p->brute;
+  c->viz = p->viz;
   c->shapes = p->shapes;
   c->num_shapes = p->num_shapes;
   int rc;
@@ -1312,7 +1360,6 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   *out = nullptr;
   kdpt_options o;
   if (opt) o = *opt; else kdpt_default_options(&o);
-  if (o.viz_kd) return fail(KDPT_ERR_UNSUPPORTED, "viz_kd (pathTraceOneBounceKDbareBoxes) is not built");
   if (o.bounce_cap <= 0) o.bounce_cap = 8;
   if (o.bounce_cap > 30) return fail(KDPT_ERR_ARG, "bounce_cap > 30");
   if (o.block_size && o.block_size != TILE) return fail(KDPT_ERR_UNSUPPORTED, "block_size must be 0 or 256");
@@ -1393,16 +1440,29 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
     return bail(fail(KDPT_ERR_HIP, "hipStreamCreate failed"));
   int rc;
-  // geoms / materials
-  std::vector<DevGeom> dg(sc->num_geoms);
-  for (int i = 0; i < sc->num_geoms; i++) {
-    dg[i].type = sc->geoms[i].type;
-    dg[i].materialid = sc->geoms[i].materialid;
-    memcpy(dg[i].transform, sc->geoms[i].transform, 64);
-    memcpy(dg[i].inverseTransform, sc->geoms[i].inverseTransform, 64);
-    memcpy(dg[i].invTranspose, sc->geoms[i].invTranspose, 64);
+  // geoms / materials (viz_kd: the KD node boxes follow the analytic geoms, as boxes with the last material,
+  // src/pathtrace.cu:1813-1831)
+  const bool viz = o.viz_kd && o.enable_kd && sc->has_obj && sc->num_nodes > 0;
+  std::vector<kdpt_geom> allg(sc->geoms, sc->geoms + sc->num_geoms);
+  if (viz) {
+    if (sc->num_materials < 1) return fail(KDPT_ERR_ARG, "viz_kd needs a material");
+    for (int k = 0; k < sc->num_nodes; k++) {
+      kdpt_geom g{};
+      g.type = 1;
+      g.materialid = sc->num_materials - 1;
+      kdpt_host::node_box_matrices(sc->nodes[k].mins, sc->nodes[k].maxs, g.transform, g.inverseTransform);
+      allg.push_back(g);
+    }
+  }
+  std::vector<DevGeom> dg(allg.size());
+  for (size_t i = 0; i < allg.size(); i++) {
+    dg[i].type = allg[i].type;
+    dg[i].materialid = allg[i].materialid;
+    memcpy(dg[i].transform, allg[i].transform, 64);
+    memcpy(dg[i].inverseTransform, allg[i].inverseTransform, 64);
+    memcpy(dg[i].invTranspose, allg[i].invTranspose, 64);
     {  // world bounds of the transformed unit cube (contains the transformed unit sphere), + margin
-      const float* m = sc->geoms[i].transform;  // column-major
+      const float* m = allg[i].transform;  // column-major
       double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
       for (int k = 0; k < 8; k++) {
         const double v[3] = {(k & 1) ? 0.5 : -0.5, (k & 2) ? 0.5 : -0.5, (k & 4) ? 0.5 : -0.5};
@@ -1446,6 +1506,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   if ((rc = dupload(c, &d_mats, dm.data(), dm.size()))) return bail(rc);
   c->S.geoms = d_geoms;
   c->S.num_geoms = sc->num_geoms;
+  c->S.num_boxes = viz ? sc->num_nodes : 0;
+  c->viz = viz;
   c->S.materials = d_mats;
   c->S.num_materials = sc->num_materials;
   c->S.has_obj = sc->has_obj ? 1 : 0;
@@ -2050,7 +2112,14 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     t.depth = depth;
     t.counters = c0->counters;
     t.trace_t = c0->trace_t;
-    if (c0->brute) {
+    if (c0->viz) {
+      for (int b = 0; b < nb; b++) {
+        kdpt_ctx* c = cs[b];
+        hipLaunchKernelGGL(k_viz, dim3(c->ntiles), dim3(TILE), 0, st, c->S, c->buf[c->cur], c->counts, depth, c->hits,
+                           c0->trace_t);
+        HIP_TRY(hipGetLastError());
+      }
+    } else if (c0->brute) {
       for (int b = 0; b < nb; b++) {
         kdpt_ctx* c = cs[b];
         BruteArgs ba;

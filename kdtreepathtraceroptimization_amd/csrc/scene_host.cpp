@@ -870,6 +870,22 @@ void obj_arrays(const kdpt_scene_desc& d, kdpt_scene_data& sd) {
 
 }  // namespace
 
+namespace kdpt_host {
+// boxIntersectionTestBox's matrices for a KD node (src/intersections.h:51-63): the unit cube scaled by
+// maxs - mins, moved to (mins + maxs) * 0.5 (double product -> float, glm::mat4's converting
+// constructor), and its glm::inverse (the same restatement the analytic geoms use).
+void node_box_matrices(const float* mins, const float* maxs, float* transform16, float* inverse16) {
+  Mat t = identity();
+  for (int a = 0; a < 3; a++) {
+    t.set(a, a, maxs[a] - mins[a]);
+    t.set(3, a, (float)((double)(mins[a] + maxs[a]) * 0.5));
+  }
+  const Mat inv = inverse(t);
+  memcpy(transform16, &t, 64);
+  memcpy(inverse16, &inv, 64);
+}
+}  // namespace kdpt_host
+
 extern "C" {
 
 int kdpt_scene_build(const kdpt_scene_desc* d, kdpt_scene_data** out) {

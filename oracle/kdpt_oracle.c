@@ -760,9 +760,52 @@ static void generateRayFromCamera(const orc_camera *cam, int iter, int traceDept
     }
 }
 
+/* boxIntersectionTestBox's transform (src/intersections.h:51-63): the node box as a unit cube scaled by
+ * maxs - mins and moved to (mins + maxs) * 0.5 (a double product, converted to float by glm::mat4's
+ * constructor), with glm::inverse; the rest of that function is boxIntersectionTest's. */
+static orc_geom node_box_geom(const orc_node *n) {
+    orc_geom g;
+    memset(&g, 0, sizeof g);
+    g.type = 1;
+    m4 t = m4identity();
+    m4set(&t, 0, 0, n->maxs[0] - n->mins[0]);
+    m4set(&t, 1, 1, n->maxs[1] - n->mins[1]);
+    m4set(&t, 2, 2, n->maxs[2] - n->mins[2]);
+    m4set(&t, 3, 0, (float)((double)(n->mins[0] + n->maxs[0]) * 0.5));
+    m4set(&t, 3, 1, (float)((double)(n->mins[1] + n->maxs[1]) * 0.5));
+    m4set(&t, 3, 2, (float)((double)(n->mins[2] + n->maxs[2]) * 0.5));
+    m4 inv = m4inverse(&t);
+    memcpy(g.transform, &t, 64);
+    memcpy(g.inverseTransform, &inv, 64);
+    return g;
+}
+
+/* The node loop of pathTraceOneBounceKDbareBoxes (vizkd, src/pathtrace.cu:1813-1831): every KD node's box
+ * as a box; a winning box reports material_size - 1 and hit_geom_index = geoms_size. */
+static void vizNodes(const orc_scene *s, const orc_geom *boxes, ray_t ray, hitrec_t *h) {
+    int outside = 1;
+    v3 tmp_i, tmp_n;
+    for (int i = 0; i < s->num_nodes; i++) {
+        float t = boxIntersectionTest(&boxes[i], ray, &tmp_i, &tmp_n, &outside);
+        if (t > 0.0f && h->t_min > t) {
+            h->t_min = t;
+            h->hit_geom_index = s->num_geoms;
+            h->intersect_point = tmp_i;
+            h->normal = tmp_n;
+            h->obj_intersect = 1;
+            h->objMaterialIdx = s->num_materials - 1;
+        }
+    }
+}
+
 /* src/pathtrace.cu:1571-1734 */
 static void traceOneBounce(const orc_scene *s, const orc_opts *o, int depth, int iter, int num_paths,
                            orc_path *paths, orc_isect *isects, counters_t *tot) {
+    orc_geom *boxes = NULL;
+    if (o->vizkd && s->has_obj) {
+        boxes = (orc_geom *)malloc(sizeof(orc_geom) * (size_t)(s->num_nodes > 0 ? s->num_nodes : 1));
+        for (int k = 0; k < s->num_nodes; k++) boxes[k] = node_box_geom(&s->nodes[k]);
+    }
     long long ca = 0, ct = 0, ch = 0;
     int nmat = s->num_materials;
 #pragma omp parallel reduction(+ : ca, ct, ch)
@@ -790,8 +833,9 @@ static void traceOneBounce(const orc_scene *s, const orc_opts *o, int depth, int
             }
             v3 bary = V3(0, 0, 0);
             if (s->has_obj) {
-                if (o->enable_kd) traverseKD(s, ray, &bary, &h, visited, o->shortstack, nmat, &cnt);
-                else bruteForceObj(s, ray, o->usebbox, &h, &cnt);
+                if (!o->enable_kd) bruteForceObj(s, ray, o->usebbox, &h, &cnt);
+                else if (o->vizkd) vizNodes(s, boxes, ray, &h);
+                else traverseKD(s, ray, &bary, &h, visited, o->shortstack, nmat, &cnt);
             }
             orc_isect *I = &isects[path_index];
             if (h.hit_geom_index == -1) {
@@ -816,6 +860,7 @@ static void traceOneBounce(const orc_scene *s, const orc_opts *o, int depth, int
         free(visited);
     }
     tot->aabb += ca; tot->tri += ct; tot->hit += ch;
+    free(boxes);
 }
 
 int orc_trace_ray(const orc_scene *s, const float *origin, const float *direction, int hybrid, double *out) {
@@ -983,6 +1028,7 @@ void orc_default_opts(orc_opts *o) {
     o->bounce_cap = 8;
     o->enable_kd = 1;
     o->usebbox = 0;
+    o->vizkd = 0;
 }
 
 int orc_render(const orc_scene *s, const orc_opts *o, int iter_first, int iter_count, float *image,

@@ -133,6 +133,7 @@ typedef struct {
     int bounce_cap;      /* 8 == the reference's hard-coded `depth > 7` (src/pathtrace.cu:2608) */
     int enable_kd;       /* 1; 0 = brute-force pathTraceOneBounce (src/pathtrace.cu:402-628) */
     int usebbox;         /* 0; brute force only: per-shape bbox test first */
+    int vizkd;           /* 0; 1 = pathTraceOneBounceKDbareBoxes (KD node boxes drawn as boxes) */
 } orc_opts;
 
 typedef struct {

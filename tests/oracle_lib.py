@@ -53,7 +53,8 @@ class OScene(C.Structure):
 class OOpts(C.Structure):
     _fields_ = [("focalLength", C.c_float), ("dofAngle", C.c_float), ("cacherays", C.c_int), ("antialias", C.c_int),
                 ("softness", C.c_float), ("enableSss", C.c_int), ("compaction", C.c_int), ("shortstack", C.c_int),
-                ("bounce_cap", C.c_int), ("enable_kd", C.c_int), ("usebbox", C.c_int)]
+                ("bounce_cap", C.c_int), ("enable_kd", C.c_int), ("usebbox", C.c_int),
+                ("vizkd", C.c_int)]
 
 
 class OStats(C.Structure):

@@ -128,3 +128,38 @@ def test_brute_force_rejects_bad_arrays(kdpt):
     opt = kdpt.default_options(enable_kd=0)
     rc = lib.kdpt_create(C.byref(view), C.byref(opt), 0, C.byref(ctx))
     assert rc == -1 and b"out of range" in lib.kdpt_last_error()
+
+
+# ---------------------------------------------------------------- viz_kd (pathTraceOneBounceKDbareBoxes)
+VIZ_CASES = [("sphere_64_viz", "sphere_low_1", (64, 64), [1, 2]), ("dragon_32_viz", "dragon_5", (32, 24), [1, 3])]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("case", VIZ_CASES, ids=[c[0] for c in VIZ_CASES])
+def test_vizkd_bit_exact_vs_oracle(kdpt, oracle, case):
+    """viz_kd draws every KD node's box as a box (src/pathtrace.cu:1738-1885): bit-exact against the oracle."""
+    _, mesh, res, iters = case
+    desc = load_fixture_scene("cornell", mesh, res=res, depth=8)
+    with kdpt.PathTracer(kdpt.SceneData.from_description(desc), kdpt.default_options(viz_kd=1), device=0) as pt:
+        segs = []
+        for it in iters:
+            pt.trace_iteration(it)
+            segs.append(pt.stats().segments)
+        g = pt.image()
+    s = oracle.OracleScene.from_description(desc)
+    o_img, o_segs = None, []
+    for it in iters:
+        im, st = s.render(it, 1, vizkd=1)
+        o_segs.append(st.segments)
+        o_img = im if o_img is None else o_img + im
+    assert segs == o_segs
+    assert np.array_equal(g.view(np.uint32), o_img.view(np.uint32))
+
+
+def test_vizkd_oracle_differs_from_kd(oracle):
+    """The box view is a different image from the traced mesh (the boxes are hit where the mesh is not)."""
+    desc = load_fixture_scene("cornell", "sphere_low_1", res=(32, 32), depth=8)
+    s = oracle.OracleScene.from_description(desc)
+    a, _ = s.render(1, 1)
+    b, _ = s.render(1, 1, vizkd=1)
+    assert not np.array_equal(a, b)
