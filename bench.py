@@ -12,16 +12,16 @@ across ranks (rank r renders global iterations r+1, r+1+N, ...: weak scaling) an
 float3 accumulation images are summed on rank 0 with one RCCL reduce over xGMI inside
 the timed region.
 
-Roofline: the dominant stage is the intersect stage (the reference's pathTraceOneBounce*): k_geoms
-(the analytic geoms and the KD root-box test; rays that miss the root box end there) then k_trace (the
-KD traversal of the rest).  HBM-bound; algorithmic bytes per segment are SURVEY.md
-8(d)'s B = 352 + 52*N_aabb + 36*N_tri + 40*N_hit restricted to the intersect kernel:
-B_trace = 76 + 52*N_aabb + 36*N_tri + 40*N_hit (PathSegment read 56 + ShadeableIntersection
-write 20, plus the tree/triangle bytes), with N_* from an untimed counting iteration; achieved =
-B_trace x segments per launch / the average stage time per bounce launch during the timed steps, measured
-on the device clock inside the kernels (first workgroup start to last workgroup end of k_geoms, plus
-the same for k_trace; agrees with rocprofv3's kernel-trace durations).  HIP events on the launching stream are reported beside it: with several
-iterations in flight they also count the time a launch waits behind the other iterations' kernels.
+Roofline: the dominant kernel is k_trace, the KD traversal of the rays that meet the KD root box (the
+analytic geoms and the root-box test of every ray run before it: in k_geoms for camera rays, fused into the
+previous bounce's shading/compaction otherwise; a ray that misses the root box ends there).  HBM-bound
+framing with SURVEY.md 8(d)'s per-segment bytes B = 352 + 52*N_aabb + 36*N_tri + 40*N_hit restricted to the
+traversal k_trace performs: per counting iteration 76*n_k + 52*(N_aabb - N_root_miss) + 36*N_tri + 40*N_hit
+(n_k = segments handed to k_trace, 76 = PathSegment read 56 + ShadeableIntersection write 20), scaled to the
+timed segments; achieved = bytes per launch / the average k_trace launch time on the device clock inside the
+kernel (first workgroup start to last workgroup end; agrees with rocprofv3's kernel-trace durations).  HIP
+events around the intersect stage are reported beside it: with several iterations in flight they also
+count the time a launch waits behind the other iterations' kernels.
 """
 from __future__ import annotations
 
@@ -35,9 +35,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # kdpt_trace_iterations keeps `--pipeline` iterations in flight on their own HIP streams plus one
 # accumulation stream; HIP's default of 4 hardware queues per process would make some of them share
-# a queue (and serialise), so ask for 8 before the runtime initialises.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
-    os.environ["GPU_MAX_HW_QUEUES"] = "8"
+# a queue (and serialise), so ask for 16 before the runtime initialises.
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
+    os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -46,8 +46,8 @@ HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=32)
-    ap.add_argument("--warmup", type=int, default=4)
+    ap.add_argument("--steps", type=int, default=192)
+    ap.add_argument("--warmup", type=int, default=8)
     ap.add_argument("--mesh", default="dragon_5")
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--res", type=int, nargs=2, default=(800, 800))
@@ -57,7 +57,7 @@ def parse():
                     help="bounces per iteration (8 = the reference's `depth > 7`; 16 for the C5 stress config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
-    ap.add_argument("--pipeline", type=int, default=3,
+    ap.add_argument("--pipeline", type=int, default=8,
                     help="batches in flight (kdpt_trace_iterations; bit-identical to one at a time)")
     ap.add_argument("--batch", type=int, default=4, help="iterations sharing each intersect launch (<= 4)")
     return ap.parse_args()
@@ -117,6 +117,10 @@ def main():
         pt.synchronize()
     # roofline counters from one untimed counting iteration of the timed range
     aabb, tri, hit = pt.count_iteration(global_iter(args.warmup))
+    try:
+        aabb_prep, cand = pt.count_split()
+    except AttributeError:  # an older libkdpt (A/B runs): no split, the whole stage
+        aabb_prep, cand = 0, None
     cnt_stats = pt.stats()
     accum.zero_()
     torch.cuda.synchronize()
@@ -154,13 +158,15 @@ def main():
         if dist:
             dist.destroy_process_group()
         return
-    # roofline of the dominant kernel (k_bounce), per launch
-    # counting iteration: aabb/tri/hit for its segments
+    # roofline of the dominant kernel, k_trace (the KD traversal of the rays that meet the root box), per
+    # launch: algorithmic bytes of the counting iteration's k_trace work, scaled to the timed segments
     count_seg = max(1, sum(cnt_stats.seg_per_bounce[d] for d in range(32)) or seg // max(1, args.steps * world))
-    per_seg_bytes = 76 + 52 * aabb / count_seg + 36 * tri / count_seg + 40 * hit / count_seg
+    cand = count_seg if cand is None else cand
+    aabb_k = aabb - aabb_prep  # the root-box tests of rays that end before k_trace are not its work
+    iter_bytes = 76 * cand + 52 * aabb_k + 36 * tri + 40 * hit
+    per_seg_bytes = iter_bytes / count_seg
     avg_launch_ms = kernel_ms / max(1, launches)
-    seg_per_launch = seg / max(1, launches)
-    bytes_per_launch = per_seg_bytes * seg_per_launch
+    bytes_per_launch = per_seg_bytes * seg / max(1, launches)
     achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
     traffic = None
     tfile = os.path.join(ROOT, "profiles", f"traffic_{args.scene}_{args.mesh}_{W}x{H}.json")
@@ -192,20 +198,27 @@ def main():
         "primary_rays_per_s": round(W * H * args.steps * world / dt, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                      "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "intersect stage = k_geoms (analytic geoms + KD root-box test, candidate list) "
-                               "+ k_trace (KD traversal of the candidates)",
+                     "kernel": "k_trace (KD traversal of the rays that meet the KD root box)",
+                     "k_trace_segments_per_launch": round(cand / count_seg * seg / max(1, launches), 1),
+                     "launch_grid_share": round(pt.trace_grid_share(), 4),
                      "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
                      "avg_launch_ms_events": round(ev_ms / max(1, ev_launches), 5),
                      "aggregate_GBps": round(per_seg_bytes * seg / dt / 1e9, 2),
                      "bytes_per_segment": round(per_seg_bytes, 2),
                      "per_segment_counts": {"aabb": round(aabb / count_seg, 4), "tri": round(tri / count_seg, 4),
-                                            "hit": round(hit / count_seg, 5)}},
+                                            "hit": round(hit / count_seg, 5),
+                                            "aabb_before_k_trace": round(aabb_prep / count_seg, 4),
+                                            "k_trace_share": round(cand / count_seg, 4)}},
         "reference_980m_intersect_ms_per_iter": 79.4,
         "intersect_ms_per_iter": round(kernel_ms / (args.steps * world), 4),
-        "timing_note": "avg_launch_ms: intersect stage per bounce launch on the device clock (s_memrealtime, first "
-                       "block start to last block end of k_geoms plus the same of k_trace), comparable with "
-                       "rocprofv3 kernel-trace durations; avg_launch_ms_events: HIP events on the launching stream "
-                       "around both, which also count queueing behind the other in-flight iterations' kernels",
+        "roofline_note": "achieved = algorithmic bytes per k_trace launch / its average duration, as the contract "
+                         "defines it; with `pipeline` batches in flight each launch runs on launch_grid_share of the "
+                         "CUs concurrently with the others, so the chip-level algorithmic rate is aggregate_GBps "
+                         "(bytes of all segments / wall time of the timed region)",
+        "timing_note": "avg_launch_ms: k_trace launches on the device clock (s_memrealtime, first block start to "
+                       "last block end), comparable with rocprofv3 kernel-trace durations; avg_launch_ms_events: HIP "
+                       "events on the launching stream around the intersect stage (k_geoms when it runs + k_trace), "
+                       "which also count queueing behind the other in-flight iterations' kernels",
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)

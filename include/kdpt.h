@@ -174,6 +174,8 @@ typedef struct kdpt_stats {
                                            last block end), summed since reset -- unlike the events,
                                            not inflated by queueing when iterations overlap */
     long long intersect_device_launches_total;
+    float intersect_grid_share;  /* fraction of the persistent intersect grid one launch used in the last
+                                    kdpt_trace_iterations (1 for one-at-a-time tracing) */
 } kdpt_stats;
 
 typedef struct kdpt_ctx kdpt_ctx;
@@ -226,6 +228,10 @@ int kdpt_debug_paths(kdpt_ctx *ctx, int iter, int stop_depth, kdpt_path_segment 
  * tests and triangle hits (aabb_tri_hit[3]); the image is not touched.  Afterwards kdpt_get_stats
  * reports that iteration's segments and seg_per_bounce. */
 int kdpt_count_iteration(kdpt_ctx *ctx, int iter, unsigned long long *aabb_tri_hit);
+/* Of the last kdpt_count_iteration: the AABB tests done before the intersect kernel (the root-box test of
+ * the rays that miss the KD root, made by k_geoms / the previous bounce's shading pass) and the number of
+ * ray segments handed to the intersect kernel (aabb_prep_cand[2]). */
+int kdpt_count_split(kdpt_ctx *ctx, unsigned long long *aabb_prep_cand);
 /* Diagnostic: cycle profile of the intersect kernel during the last kdpt_count_iteration.
  * Copies up to n values -- node trips, node cycles, big-leaf sweeps, big-leaf cycles,
  * small-leaf phases, small-leaf rounds, small-leaf cycles, recombination cycles, setup

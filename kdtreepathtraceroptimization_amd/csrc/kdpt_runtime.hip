@@ -64,6 +64,8 @@ struct PathBuf {
 
 struct Counters {
   unsigned long long aabb, tri, hit;
+  unsigned long long aabb_prep;  // root-box tests of rays that end before the intersect kernel (k_geoms/k_shade)
+  unsigned long long cand;       // rays handed to the intersect kernel
   unsigned long long wave[PROF_SLOTS + 2];  // WaveLeafLDS::prof summed over chunks, then chunks, cycles
   unsigned long long life[64];  // count mode: wave lifetimes in the intersect kernel, 10 us bins (s_memrealtime)
 };
@@ -148,6 +150,9 @@ __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int
 // ---------------------------------------------------------------------------
 enum TreeMode { TREE_WIDE = 0, TREE_PACKED = 1, TREE_LDS = 2 };
 constexpr int TRACE_BLOCK = 1024;  // LDS mode: one workgroup per CU shares the tree copy
+#ifndef KDPT_SRUN_SPREAD
+#define KDPT_SRUN_SPREAD 0  // 1: static runs of ceil(n / waves) instead of 64 (experiment)
+#endif
 // workgroup size of the intersect kernel: with the tree in LDS every wave of a CU must share the copy,
 // otherwise small workgroups let the tail of one launch hold only a quarter of a CU
 template <int MODE>
@@ -196,6 +201,41 @@ __device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, 
   }
 }
 
+// The intersect stage's first part for one ray: the analytic geoms of pathTraceOneBounceKDbare (tested
+// before the KD tree; src/pathtrace.cu:1600-1640) -> t_min / hit, and the traversal's first step, the
+// KD root's box (same intersectAABB, same invdir): false = the traversal ends there.
+__device__ inline bool prep_ray(const DevScene& S, bool kd, f3 o, f3 d, float& t_min, int& hit) {
+  Ray ray;
+  ray.origin = o;
+  ray.direction = d;
+  ray.isinside = false;
+  ray.sdepth = 0.0f;
+  t_min = FLT_MAXV;
+  hit = -1;
+  f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
+  float t = 0;
+  const f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const bool finite = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
+  for (int g = 0; g < S.num_geoms; g++) {
+    const DevGeom& G = S.geoms[g];
+    if (finite && !geom_may_hit(G, o, inv)) {
+      t = -1.0f;  // the exact test would miss
+    } else if (G.type == 1) {
+      t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
+    } else if (G.type == 0) {
+      t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+    }
+    if (t > 0.0f && t_min > t) {
+      t_min = t;
+      hit = g;
+    }
+  }
+  if (!kd) return false;
+  float dist;
+  return intersectAABB(o, inv, make_float4(S.rlo.x, S.rlo.y, S.rlo.z, S.rhi.x),
+                       make_float4(S.rhi.y, S.rhi.z, 0.0f, 0.0f), dist);
+}
+
 // The analytic geoms of pathTraceOneBounceKDbare (tested before the KD tree; src/pathtrace.cu:1600-1640),
 // one lane per live path, consecutive paths per wave: {t_min bits, geom index} for k_trace.
 //
@@ -217,37 +257,10 @@ __global__ __launch_bounds__(GEOM_BLOCK) void k_geoms(DevScene S, PathBuf paths,
   // finished paths (compaction off) are skipped, as pathTraceOneBounce* skips them
   if (i < n && fbits(paths.p2[i].w) > 0) {
     const float4 q0 = paths.p0[i], q1 = paths.p1[i];
-    Ray ray;
-    ray.origin = mk3(q0.x, q0.y, q0.z);
-    ray.direction = mk3(q1.x, q1.y, q1.z);
-    ray.isinside = false;
-    ray.sdepth = q0.w;
-    float t_min = FLT_MAXV;
-    int hit = -1;
-    f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
-    float t = 0;
-    const f3 inv = mk3(1.0f / ray.direction.x, 1.0f / ray.direction.y, 1.0f / ray.direction.z);
-    const bool finite = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
-    for (int g = 0; g < S.num_geoms; g++) {
-      const DevGeom& G = S.geoms[g];
-      if (finite && !geom_may_hit(G, ray.origin, inv)) {
-        t = -1.0f;  // the exact test would miss
-      } else if (G.type == 1) {
-        t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
-      } else if (G.type == 0) {
-        t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
-      }
-      if (t > 0.0f && t_min > t) {
-        t_min = t;
-        hit = g;
-      }
-    }
-    if (kd) {  // the traversal's first step: the root's box (same intersectAABB, same invdir)
-      float dist;
-      tested = true;
-      walk = intersectAABB(ray.origin, inv, make_float4(S.rlo.x, S.rlo.y, S.rlo.z, S.rhi.x),
-                           make_float4(S.rhi.y, S.rhi.z, 0.0f, 0.0f), dist);
-    }
+    float t_min;
+    int hit;
+    tested = kd;
+    walk = prep_ray(S, kd, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z), t_min, hit);
     if (walk) geomhit[i] = make_int2(fbits(t_min), hit);
     else hits[i] = make_int2(hit, -1);  // final: the analytic geoms' hit (code -1: none)
   }
@@ -257,9 +270,13 @@ __global__ __launch_bounds__(GEOM_BLOCK) void k_geoms(DevScene S, PathBuf paths,
   const unsigned long long wm = __ballot(walk);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) s_wcount[wv] = __popcll(wm);
-  if (count_aabb) {  // count mode: the root test of the rays that end here
+  if (count_aabb) {  // count mode: the root test of the rays that end here, and the candidates
     const unsigned long long miss = __ballot(tested && !walk);
-    if (lane == 0 && miss) atomicAdd(&count_aabb->aabb, (unsigned long long)__popcll(miss));
+    if (lane == 0 && miss) {
+      atomicAdd(&count_aabb->aabb, (unsigned long long)__popcll(miss));
+      atomicAdd(&count_aabb->aabb_prep, (unsigned long long)__popcll(miss));
+    }
+    if (lane == 0 && wm) atomicAdd(&count_aabb->cand, (unsigned long long)__popcll(wm));
   }
   __syncthreads();
   if (threadIdx.x == 0) {
@@ -321,13 +338,14 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
   R.done = true;
   int pidx = -1;  // the lane's path (-1: idle)
   int pb = 0;     // ... and the batch iteration it belongs to
-  // Path slots: each wave first takes a static run of ceil(n / nwaves) (at most 64) consecutive slots,
-  // so that every CU gets work even when a bounce has few rays (the kernel is issue-bound: rays piled
-  // onto a few CUs would leave the others idle); a device counter hands out the rest, exactly as many
-  // as the wave has idle lanes, so the tail of the bounce stays balanced.
+  // Path slots: each wave first takes a static run of 64 consecutive slots, the runs dealt out wave-major
+  // across the workgroups (run r goes to wave r / grid of workgroup r % grid): a bounce with few rays then
+  // still fills every CU (the kernel is issue-bound: rays piled onto a few CUs would leave the others idle)
+  // while each wave stays dense (a node trip costs the same whatever the number of walking lanes).  A device
+  // counter hands out the rest, exactly as many as the wave has idle lanes, so the tail stays balanced.
   const int nwaves = gridDim.x * (TB / 64);
-  const int wid = blockIdx.x * (TB / 64) + (threadIdx.x >> 6);
-  const int srun = min(64, max(1, (n + nwaves - 1) / nwaves));
+  const int wid = (threadIdx.x >> 6) * gridDim.x + blockIdx.x;
+  const int srun = KDPT_SRUN_SPREAD ? min(64, max(1, (n + nwaves - 1) / nwaves)) : 64;
   bool first = true, exhausted = false;
   long long rounds = 0;
   while (true) {
@@ -647,6 +665,12 @@ struct ShadeArgs {
   const unsigned long long* trace_t;   // this bounce's intersect launch record (see TraceArgs)
   const unsigned long long* gspan;     // ... and the k_geoms launches' record
   unsigned long long* trace_total;     // [2]: summed launch ticks, launches
+  // next bounce's intersect-stage first part (prep_ray) for every surviving path, fused here instead of a
+  // k_geoms pass: {t_min bits, (geom + 1) | walks << 16} at the path's current slot (k_scatter moves it)
+  int prep_on;
+  int2* prep;
+  int* tile_ccounts;   // [ntiles] walking survivors per tile
+  Counters* count_aabb;  // count mode: root tests of the rays that end there
 };
 
 template <bool HYBRID, bool COMPACT, bool SORT>
@@ -657,11 +681,10 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   const int i = tile * TILE + threadIdx.x;
   if (i == 0) {
     atomicAdd(A.total_segments, (unsigned long long)n);
-    // the intersect stage of this bounce on the device clock: k_geoms' span + k_trace's span (a kernel
-    // that had nothing to do left its record empty)
+    // the intersect kernel of this bounce on the device clock (first block start .. last block end; a
+    // launch that had nothing to do left its record empty)
     const unsigned long long t0 = A.trace_t[2 * A.depth], t1 = A.trace_t[2 * A.depth + 1];
-    const unsigned long long g0 = A.gspan[2 * A.depth], g1 = A.gspan[2 * A.depth + 1];
-    const unsigned long long span = (t1 > t0 ? t1 - t0 : 0ull) + (g1 > g0 ? g1 - g0 : 0ull);
+    const unsigned long long span = t1 > t0 ? t1 - t0 : 0ull;
     if (A.trace_total && span) {
       atomicAdd(&A.trace_total[0], span);
       atomicAdd(&A.trace_total[1], 1ull);
@@ -675,7 +698,7 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   if (COMPACT && A.tile_kcounts && threadIdx.x < TRACE_KEYS) s_khist[threadIdx.x] = 0;
   if (SORT || (COMPACT && A.tile_kcounts)) __syncthreads();
   const DevScene& S = A.S;
-  bool alive = false;
+  bool alive = false, walk = false, tested = false;
   int key = 0;
   if (i < n) {
     const float4 q0 = A.paths.p0[i], q1 = A.paths.p1[i], q2 = A.paths.p2[i];
@@ -730,6 +753,13 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
     }
     alive = COMPACT ? (bounces != 0) : true;
     key = matHit;
+    if (COMPACT && A.prep_on && bounces != 0) {
+      float tm;
+      int gh;
+      walk = prep_ray(S, S.has_obj && S.num_nodes > 0, ray.origin, ray.direction, tm, gh);
+      tested = S.has_obj && S.num_nodes > 0;
+      A.prep[i] = make_int2(fbits(tm), (gh + 1) | (walk ? 0x10000 : 0));
+    }
     if (COMPACT && A.tile_kcounts && alive) atomicAdd(&s_khist[trace_class(S, ray.origin, ray.direction)], 1);
   }
   if (COMPACT && A.tile_kcounts) {
@@ -744,11 +774,24 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
     const int c = __syncthreads_count(alive);
     if (threadIdx.x == 0) A.tile_counts[tile] = c;
   }
+  if (COMPACT && A.prep_on) {
+    const int cw = __syncthreads_count(walk);
+    if (threadIdx.x == 0) A.tile_ccounts[tile] = cw;
+    if (A.count_aabb) {
+      const unsigned long long miss = __ballot(tested && !walk), wm = __ballot(walk);
+      if ((threadIdx.x & 63) == 0 && miss) {
+        atomicAdd(&A.count_aabb->aabb, (unsigned long long)__popcll(miss));
+        atomicAdd(&A.count_aabb->aabb_prep, (unsigned long long)__popcll(miss));
+      }
+      if ((threadIdx.x & 63) == 0 && wm) atomicAdd(&A.count_aabb->cand, (unsigned long long)__popcll(wm));
+    }
+  }
 }
 
 // Exclusive scan of the tile counts (one workgroup; <= MAX_KEYS * ntiles entries).
 __global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ tile_counts, int* __restrict__ tile_off,
-                                               int* counts, int depth, int ntiles_alloc, int nkeys, int write_total) {
+                                               const int* counts, int depth, int ntiles_alloc, int nkeys,
+                                               int* total_out) {
   const int n = counts[depth];
   const int ntiles = (n + TILE - 1) / TILE;
   const int total_entries = nkeys * ntiles;
@@ -790,20 +833,32 @@ __global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ tile_coun
     if (threadIdx.x == 1023) s_carry = excl + v;
     __syncthreads();
   }
-  if (threadIdx.x == 0 && write_total) counts[depth + 1] = s_carry;
+  if (threadIdx.x == 0 && total_out) *total_out = s_carry;
 }
 
 // Stable compaction (and, on iter 2, the stable sort by materialIdHit).
+// The next bounce's intersect-stage hand-off, moved with the survivors by k_scatter: walking rays get their
+// geoms record at the new slot and a candidate-list entry (stable: tile order, offsets from k_scan), the
+// others their final hit record.
+struct ScatterPrep {
+  int on;
+  const int2* prep;
+  int2* geomhit;
+  int2* hits;
+  int* cand;
+  const int* tile_coff;
+};
+
 template <bool SORT>
 __global__ __launch_bounds__(TILE) void k_scatter(PathBuf src, PathBuf dst, const int* __restrict__ tile_off,
                                                   const int* counts, int depth, int ntiles_alloc, int compact,
-                                                  const int* __restrict__ ktile_off, int* __restrict__ perm,
-                                                  DevScene S) {
+                                                  ScatterPrep P) {
   const int n = counts[depth];
   const int tile = blockIdx.x;
   if (tile * TILE >= n) return;
   const int i = tile * TILE + threadIdx.x;
   const bool valid = i < n;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   float4 q0, q1, q2;
   int pm = 0;
   bool alive = false;
@@ -818,7 +873,6 @@ __global__ __launch_bounds__(TILE) void k_scatter(PathBuf src, PathBuf dst, cons
   if (!SORT) {
     __shared__ int s_wave[TILE / 64];
     const unsigned long long m = __ballot(alive);
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     if (lane == 0) s_wave[wid] = __popcll(m);
     __syncthreads();
     int before = 0;
@@ -838,26 +892,23 @@ __global__ __launch_bounds__(TILE) void k_scatter(PathBuf src, PathBuf dst, cons
     dst.p2[dst_i] = q2;
     dst.pm[dst_i] = pm;
   }
-  if (perm) {
-    // next bounce's trace order: stable by trace_class (the keys k_shade counted), tile-major
-    __shared__ int s_kc[TILE / 64][TRACE_KEYS];
-    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
-    for (int k = lane; k < TRACE_KEYS; k += 64) s_kc[wid][k] = 0;
-    const int key = alive ? trace_class(S, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z)) : 0;
-    int rank = 0;
-    unsigned long long rem = __ballot(alive);
-    while (rem) {  // one round per distinct key in the wave
-      const int k = __shfl(key, __builtin_ctzll(rem));
-      const unsigned long long m = __ballot(alive && key == k);
-      if (alive && key == k) rank = (int)lane_prefix(m);
-      if (lane == 0) s_kc[wid][k] = __popcll(m);
-      rem &= ~m;
-    }
+  if (P.on) {
+    __shared__ int s_walk[TILE / 64];
+    const int2 pr = alive ? P.prep[i] : make_int2(0, 0);
+    const bool w = alive && (pr.y & 0x10000);
+    const int geom = (pr.y & 0xffff) - 1;
+    const unsigned long long m = __ballot(w);
+    if (lane == 0) s_walk[wid] = __popcll(m);
     __syncthreads();
     if (alive) {
-      int before = 0;
-      for (int w = 0; w < wid; w++) before += s_kc[w][key];
-      perm[ktile_off[key * ntiles_alloc + tile] + before + rank] = dst_i;
+      if (w) {
+        int before = 0;
+        for (int k = 0; k < wid; k++) before += s_walk[k];
+        P.geomhit[dst_i] = make_int2(pr.x, geom);
+        P.cand[P.tile_coff[tile] + before + (int)lane_prefix(m)] = dst_i;
+      } else {
+        P.hits[dst_i] = make_int2(geom, -1);  // final: the analytic geoms' hit (code -1: none)
+      }
     }
   }
 }
@@ -970,9 +1021,13 @@ struct kdpt_ctx {
   int2* hits = nullptr;   // [npix] hit code + objMaterialIdx from the intersect kernel
   int2* geomhit = nullptr;  // [npix] analytic-geom t_min bits + index (k_geoms -> k_trace)
   int* cand = nullptr;      // [npix] paths whose ray meets the KD root box (k_geoms -> k_trace)
+  int2* prep = nullptr;     // [npix] next bounce's geoms record + walk flag (k_shade -> k_scatter)
+  int* tile_ccounts = nullptr;  // [ntiles] walking survivors per tile, and their offsets
+  int* tile_coff = nullptr;
   int* ccount = nullptr;    // [cap] their number per bounce (inside the counts allocation)
   int tree_mode = 0;      // TreeMode
   int trace_grid = 0;     // persistent intersect workgroups
+  bool grid_env = false;  // trace_grid fixed by KDPT_TRACE_GRID_FRAC
   size_t tree_lds = 0;    // dynamic LDS bytes of the intersect kernel (TREE_LDS)
   int* tile_counts = nullptr;
   int* tile_off = nullptr;
@@ -1071,7 +1126,8 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
   if ((rc = dalloc(c, &c->trace_t, 4 * (size_t)c->cap))) return rc;
   HIP_TRY(hipMemset(c->trace_t, 0, sizeof(unsigned long long) * 4 * c->cap));
   if ((rc = dalloc(c, &c->counts, 3 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
-      (rc = dalloc(c, &c->cand, (size_t)c->npix)) ||
+      (rc = dalloc(c, &c->cand, (size_t)c->npix)) || (rc = dalloc(c, &c->prep, (size_t)c->npix)) ||
+      (rc = dalloc(c, &c->tile_ccounts, (size_t)c->ntiles)) || (rc = dalloc(c, &c->tile_coff, (size_t)c->ntiles)) ||
       (rc = dalloc(c, &c->geomhit, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->perm, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->tile_kcounts, (size_t)TRACE_KEYS * c->ntiles)) ||
@@ -1314,6 +1370,13 @@ int setup_trace(kdpt_ctx* c) {
   if (rc) return rc;
   if (blocks < 1) return fail(KDPT_ERR_UNSUPPORTED, "intersect kernel does not fit on a CU");
   c->trace_grid = blocks * prop.multiProcessorCount;
+  if (const char* gf = getenv("KDPT_TRACE_GRID_FRAC")) {  // experiment: a fixed fraction of the grid
+    const double f = atof(gf);
+    if (f > 0.0 && f <= 1.0) {
+      c->trace_grid = std::max(1, (int)(c->trace_grid * f));
+      c->grid_env = true;
+    }
+  }
   return KDPT_OK;
 }
 
@@ -1670,6 +1733,7 @@ int kdpt_reset(kdpt_ctx* c) {
   HIP_TRY(hipMemsetAsync(c->trace_total, 0, 2 * sizeof(unsigned long long), c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   memset(&c->stats, 0, sizeof c->stats);
+  c->stats.intersect_grid_share = 1.0f;
   return KDPT_OK;
 }
 
@@ -1767,6 +1831,12 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
     }
   }
   const int ngroups = (int)c->slot_done.size();
+  // With several batches in flight each intersect launch gets a share of the chip (2/depth of the
+  // persistent grid, all of it for depth <= 2): a launch's length is set by its heaviest rays, so
+  // concurrent launches on disjoint CU subsets overlap those tails instead of queueing behind them.
+  for (auto sl : c->slots)
+    sl->trace_grid = c->grid_env ? c->trace_grid : std::max(1, c->trace_grid * 2 / std::max(2, depth));
+  c->stats.intersect_grid_share = c->slots.empty() ? 1.0f : (float)c->slots[0]->trace_grid / (float)c->trace_grid;
   {  // diagnostic: KDPT_PROFILE_BATCHES=1 runs the counting intersect kernel (kdpt_wave_profile after sync)
     const char* e = getenv("KDPT_PROFILE_BATCHES");
     c->profile_batches = e && e[0] == '1';
@@ -1993,6 +2063,13 @@ int kdpt_count_iteration(kdpt_ctx* c, int iter, unsigned long long* aabb_tri_hit
   return rc;
 }
 
+int kdpt_count_split(kdpt_ctx* c, unsigned long long* aabb_prep_cand) {
+  if (!c || !aabb_prep_cand) return fail(KDPT_ERR_ARG, "null arg");
+  aabb_prep_cand[0] = c->last_profile.aabb_prep;
+  aabb_prep_cand[1] = c->last_profile.cand;
+  return KDPT_OK;
+}
+
 int kdpt_wave_profile(kdpt_ctx* c, unsigned long long* out, int n) {
   if (!c || !out) return fail(KDPT_ERR_ARG, "null arg");
   unsigned long long v[PROF_SLOTS + 5];
@@ -2095,7 +2172,9 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     HIP_TRY(hipGetLastError());
   }
   const bool compact = c0->opt.compaction != 0;
+  bool prep_ready = false;  // this bounce's intersect-stage first part came with the previous scatter
   for (int depth = 0; depth < c0->cap; depth++) {
+    const bool prep_next = compact && depth + 1 < c0->cap && !c0->brute && !c0->viz;
     if (c0->opt.testing_mode && bev) HIP_TRY(hipEventRecord((*bev)[2 * depth], st));
     TraceArgs t;
     t.S = c0->S;
@@ -2150,7 +2229,9 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         }
       }
     } else {
-      for (int b = 0; b < nb; b++) {
+      // the intersect stage's first part: already done by the previous bounce's k_shade/k_scatter when it
+      // ran with the hand-off (prep_ready), else here
+      for (int b = 0; b < nb && !prep_ready; b++) {
         kdpt_ctx* c = cs[b];
         hipLaunchKernelGGL(k_geoms, dim3((c->npix + GEOM_BLOCK - 1) / GEOM_BLOCK), dim3(GEOM_BLOCK), 0, st, c->S,
                            c->buf[c->cur], c->counts, depth,
@@ -2189,28 +2270,31 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       a.trace_t = c0->trace_t;
       a.gspan = c0->trace_t + 2 * c0->cap;
       a.trace_total = b == 0 ? c->trace_total : nullptr;
+      a.prep_on = prep_next ? 1 : 0;
+      a.prep = c->prep;
+      a.tile_ccounts = c->tile_ccounts;
+      a.count_aabb = count ? c0->counters : nullptr;
       // hit point offset: 1e-4 for the hybrid traversal and the brute-force kernel, 1e-5 for traverseKDbare
       if (c->opt.short_stack || c->brute) launch_shade_h<true>(c, a, compact, sort, st);
       else launch_shade_h<false>(c, a, compact, sort, st);
       HIP_TRY(hipGetLastError());
       if (compact || sort) {
         hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, c->tile_counts, c->tile_off, c->counts, depth,
-                           c->ntiles, sort ? c->nkeys : 1, 1);
+                           c->ntiles, sort ? c->nkeys : 1, c->counts + depth + 1);
         HIP_TRY(hipGetLastError());
-        const bool order = compact && c->trace_order;
-        if (order) {
-          hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, c->tile_kcounts, c->tile_koff, c->counts, depth,
-                             c->ntiles, TRACE_KEYS, 0);
+        if (prep_next) {  // candidate-list offsets per tile and the next bounce's candidate count
+          hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, c->tile_ccounts, c->tile_coff, c->counts, depth,
+                             c->ntiles, 1, c->ccount + depth + 1);
           HIP_TRY(hipGetLastError());
         }
         const int nxt = c->cur ^ 1;
-        int* perm = order ? c->perm : nullptr;
+        ScatterPrep sp{prep_next ? 1 : 0, c->prep, c->geomhit, c->hits, c->cand, c->tile_coff};
         if (sort)
           hipLaunchKernelGGL(k_scatter<true>, dim3(c->ntiles), dim3(TILE), 0, st, c->buf[c->cur], c->buf[nxt],
-                             c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, c->tile_koff, perm, c->S);
+                             c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, sp);
         else
           hipLaunchKernelGGL(k_scatter<false>, dim3(c->ntiles), dim3(TILE), 0, st, c->buf[c->cur], c->buf[nxt],
-                             c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, c->tile_koff, perm, c->S);
+                             c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, sp);
         HIP_TRY(hipGetLastError());
         c->cur = nxt;
       } else {
@@ -2223,6 +2307,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       fprintf(stderr, "[kdpt] shade depth %d done\n", depth);
     }
     if (stop_depth == depth) return KDPT_OK;
+    prep_ready = prep_next;
   }
   if (!compact) {
     for (int b = 0; b < nb; b++) {

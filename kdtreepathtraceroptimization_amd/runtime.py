@@ -89,7 +89,7 @@ class Stats(C.Structure):
                 ("iterations", C.c_int), ("ms_last_iteration", C.c_float), ("ms_intersect", C.c_float),
                 ("total_segments", C.c_longlong), ("intersect_ms_total", C.c_double),
                 ("intersect_launches_total", C.c_longlong), ("intersect_device_ms_total", C.c_double),
-                ("intersect_device_launches_total", C.c_longlong)]
+                ("intersect_device_launches_total", C.c_longlong), ("intersect_grid_share", C.c_float)]
 
 
 class SceneDesc(C.Structure):
@@ -108,7 +108,7 @@ assert C.sizeof(NodeBare) == 64 and C.sizeof(TriBare) == 76 and C.sizeof(PathSeg
 EXPORTS = [
     "kdpt_default_options", "kdpt_create", "kdpt_trace_iteration", "kdpt_trace_iteration_async", "kdpt_trace_iterations", "kdpt_synchronize",
     "kdpt_read_image", "kdpt_write_pbo", "kdpt_reset", "kdpt_get_stats", "kdpt_destroy", "kdpt_last_error",
-    "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_wave_profile", "kdpt_selftest_math", "kdpt_selftest_rng",
+    "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_count_split", "kdpt_wave_profile", "kdpt_selftest_math", "kdpt_selftest_rng",
     "kdpt_selftest_fresnel", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
     "kdpt_save_rgb8", "kdpt_save_png", "kdpt_save_hdr", "kdpt_png_encode", "kdpt_write_png", "kdpt_hdr_encode",
     "kdpt_write_hdr", "kdpt_free",
@@ -147,6 +147,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_image_device_ptr.argtypes = [C.c_void_p, P(C.c_void_p)]
     lib.kdpt_debug_paths.argtypes = [C.c_void_p, C.c_int, C.c_int, P(PathSegment), P(C.c_int)]
     lib.kdpt_count_iteration.argtypes = [C.c_void_p, C.c_int, P(C.c_ulonglong)]
+    if hasattr(lib, "kdpt_count_split"):  # diagnostic; absent from older builds used in A/B runs
+        lib.kdpt_count_split.argtypes = [C.c_void_p, P(C.c_ulonglong)]
     lib.kdpt_wave_profile.argtypes = [C.c_void_p, P(C.c_ulonglong), C.c_int]
     lib.kdpt_selftest_math.argtypes = [P(C.c_float), C.c_int, P(C.c_float), P(C.c_float)]
     lib.kdpt_selftest_rng.argtypes = [P(C.c_int), C.c_int, C.c_int, P(C.c_float)]
@@ -420,6 +422,15 @@ class PathTracer:
         out = (C.c_ulonglong * 3)()
         _check(self.lib.kdpt_count_iteration(self._ctx, int(iteration), out), "kdpt_count_iteration")
         return int(out[0]), int(out[1]), int(out[2])
+
+    def trace_grid_share(self) -> float:
+        return float(self.stats().intersect_grid_share)
+
+    def count_split(self):
+        """(AABB tests made before the intersect kernel, segments handed to it) of the last count_iteration."""
+        out = (C.c_ulonglong * 2)()
+        _check(self.lib.kdpt_count_split(self._ctx, out), "kdpt_count_split")
+        return int(out[0]), int(out[1])
 
     def wave_profile(self):
         """Cycle profile of the intersect kernel in the last count_iteration (kdpt_wave_profile)."""

@@ -186,7 +186,7 @@ def test_soft_branch_within_tolerance(kdpt, oracle, opts):
     assert same > 0.99, same
 
 
-@pytest.mark.parametrize("pipeline,batch", [(1, 1), (3, 1), (2, 3), (1, 4)])
+@pytest.mark.parametrize("pipeline,batch", [(1, 1), (3, 1), (2, 3), (1, 4), (8, 4), (5, 2)])
 def test_pipelined_iterations_bit_exact(kdpt, pipeline, batch):
     """kdpt_trace_iterations (batches sharing intersect launches, several batches in flight, partial
     images added in order) gives the same image bits and segment counts as one kdpt_trace_iteration
@@ -194,13 +194,14 @@ def test_pipelined_iterations_bit_exact(kdpt, pipeline, batch):
     desc = load_fixture_scene("cornell", "dragon_5", res=(96, 80), depth=8)
     sd = kdpt.SceneData.from_description(desc)
     seq = kdpt.PathTracer(sd, kdpt.default_options())
-    for it in range(1, 8):
+    n_it = max(7, pipeline * batch + 3)  # enough to wrap around every slot group
+    for it in range(1, n_it + 1):
         seq.trace_iteration(it)
     img_seq = seq.image()
     tot_seq = seq.stats().total_segments
     seq.close()
     pip = kdpt.PathTracer(sd, kdpt.default_options())
-    pip.trace_iterations(1, 7, pipeline=pipeline, batch=batch)
+    pip.trace_iterations(1, n_it, pipeline=pipeline, batch=batch)
     pip.synchronize()
     img_pip = pip.image()
     tot_pip = pip.stats().total_segments

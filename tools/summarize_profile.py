@@ -30,21 +30,16 @@ def main():
     for r in rows:
         out["kernels"][r["Name"][:90]] = {"calls": int(r["Calls"]), "avg_ms": float(r["AverageNs"]) / 1e6,
                                           "pct": float(r["Percentage"])}
-    # the intersect stage of one bounce = the batch's k_geoms launches + one k_trace launch: all their
-    # bytes over the number of k_trace launches
     fpath = os.path.join(src, "pmc_fetch", "run_counter_collection.csv")
     wpath = os.path.join(src, "pmc_write", "run_counter_collection.csv")
-    fetch_t, write_t = per_dispatch(fpath, "FETCH_SIZE", "k_trace"), per_dispatch(wpath, "WRITE_SIZE", "k_trace")
-    fetch_g, write_g = per_dispatch(fpath, "FETCH_SIZE", "k_geoms"), per_dispatch(wpath, "WRITE_SIZE", "k_geoms")
-    if fetch_t and write_t:
-        f = 2.0 * 1024 * (sum(fetch_t) + sum(fetch_g)) / len(fetch_t)  # KB -> B, x2 gfx950 FETCH_SIZE correction
-        w = 1024 * (sum(write_t) + sum(write_g)) / len(write_t)
-        out["intersect_stage_hbm_bytes_per_launch"] = {"fetch": f, "write": w, "total": f + w,
-                                                       "k_trace_launches": len(fetch_t),
-                                                       "k_geoms_launches": len(fetch_g)}
+    fetch, write = per_dispatch(fpath, "FETCH_SIZE", "k_trace"), per_dispatch(wpath, "WRITE_SIZE", "k_trace")
+    if fetch and write:
+        f = 2.0 * 1024 * sum(fetch) / len(fetch)  # KB -> B, x2 gfx950 FETCH_SIZE correction
+        w = 1024 * sum(write) / len(write)
+        out["k_trace_hbm_bytes_per_launch"] = {"fetch": f, "write": w, "total": f + w, "launches": len(fetch)}
         tfile = os.path.join(os.path.dirname(dst), f"traffic_{scene}_{mesh}_{res}.json")
-        json.dump({"kernel": "intersect stage (k_geoms + k_trace)", "hbm_bytes_per_launch": round(f + w),
-                   "fetch_bytes": round(f), "write_bytes": round(w), "launches": len(fetch_t),
+        json.dump({"kernel": "k_trace", "hbm_bytes_per_launch": round(f + w),
+                   "fetch_bytes": round(f), "write_bytes": round(w), "launches": len(fetch),
                    "source": os.path.basename(dst) + " (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE, separate passes)"},
                   open(tfile, "w"), indent=1)
     json.dump(out, open(dst + "_summary.json", "w"), indent=1)
