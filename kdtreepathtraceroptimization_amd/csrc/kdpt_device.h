@@ -66,6 +66,20 @@ KDPT_HD bool geom_may_hit(const DevGeom& G, f3 o, f3 invdir) {
   return tmax >= tmin && tmax >= 0.0f;
 }
 
+// Entry distance of the ray into the geom's enlarged world bounds: a lower bound of the exact test's t
+// whenever that test hits (the bounds' margin, >= 1e-3 x extent + 1e-3, exceeds the exact test's 1e-4
+// pull-back along the object-space direction, <= 1e-4 x the largest scale, plus rounding).  false: the
+// exact test would miss (as geom_may_hit).
+KDPT_HD bool geom_entry_bound(const DevGeom& G, f3 o, f3 invdir, float& lo) {
+  const float t1x = (G.wlo[0] - o.x) * invdir.x, t2x = (G.whi[0] - o.x) * invdir.x;
+  const float t1y = (G.wlo[1] - o.y) * invdir.y, t2y = (G.whi[1] - o.y) * invdir.y;
+  const float t1z = (G.wlo[2] - o.z) * invdir.z, t2z = (G.whi[2] - o.z) * invdir.z;
+  const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
+  const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+  lo = tmin;
+  return tmax >= tmin && tmax >= 0.0f;
+}
+
 struct DevScene {
   const DevGeom* geoms;
   int num_geoms;

@@ -204,6 +204,7 @@ __device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, 
 // The intersect stage's first part for one ray: the analytic geoms of pathTraceOneBounceKDbare (tested
 // before the KD tree; src/pathtrace.cu:1600-1640) -> t_min / hit, and the traversal's first step, the
 // KD root's box (same intersectAABB, same invdir): false = the traversal ends there.
+constexpr int ORDERED_GEOMS = 8;  // scenes with at most this many analytic geoms test them nearest-first
 __device__ inline bool prep_ray(const DevScene& S, bool kd, f3 o, f3 d, float& t_min, int& hit) {
   Ray ray;
   ray.origin = o;
@@ -213,21 +214,55 @@ __device__ inline bool prep_ray(const DevScene& S, bool kd, f3 o, f3 d, float& t
   t_min = FLT_MAXV;
   hit = -1;
   f3 tmp_i = mk3(0, 0, 0), tmp_n = mk3(0, 0, 0);
-  float t = 0;
   const f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
   const bool finite = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
-  for (int g = 0; g < S.num_geoms; g++) {
-    const DevGeom& G = S.geoms[g];
-    if (finite && !geom_may_hit(G, o, inv)) {
-      t = -1.0f;  // the exact test would miss
-    } else if (G.type == 1) {
-      t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
-    } else if (G.type == 0) {
-      t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+  const int ng = S.num_geoms;
+  if (finite && ng <= ORDERED_GEOMS) {
+    // Nearest-first: the reference keeps the first geom (index order) reaching the smallest t > 0; here
+    // the geoms whose bounds the ray enters are tested in order of their entry bound, stopping once that
+    // bound exceeds the best t, and ties go to the lower index -- the same winner and the same t, with
+    // typically one or two exact tests per ray instead of one per geom the wave's rays come near.
+    float lo[ORDERED_GEOMS];
+    uint32_t pending = 0;
+#pragma unroll
+    for (int g = 0; g < ORDERED_GEOMS; g++) {
+      lo[g] = FLT_INFV;
+      if (g < ng && geom_entry_bound(S.geoms[g], o, inv, lo[g])) pending |= 1u << g;
     }
-    if (t > 0.0f && t_min > t) {
-      t_min = t;
-      hit = g;
+    while (pending) {
+      int gb = 0;
+      float lb = FLT_INFV;
+#pragma unroll
+      for (int g = 0; g < ORDERED_GEOMS; g++)
+        if (((pending >> g) & 1u) && lo[g] < lb) {
+          lb = lo[g];
+          gb = g;
+        }
+      if (lb > t_min) break;  // every remaining geom's exact t exceeds the best
+      pending &= ~(1u << gb);
+      const DevGeom& G = S.geoms[gb];
+      const float t = G.type == 1 ? boxIntersectionTest(G, ray, tmp_i, tmp_n)
+                                  : sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+      if (t > 0.0f && (t < t_min || (t == t_min && gb < hit))) {
+        t_min = t;
+        hit = gb;
+      }
+    }
+  } else {
+    float t = 0;
+    for (int g = 0; g < ng; g++) {
+      const DevGeom& G = S.geoms[g];
+      if (finite && !geom_may_hit(G, o, inv)) {
+        t = -1.0f;  // the exact test would miss
+      } else if (G.type == 1) {
+        t = boxIntersectionTest(G, ray, tmp_i, tmp_n);
+      } else if (G.type == 0) {
+        t = sphereIntersectionTest(G, ray, tmp_i, tmp_n);
+      }
+      if (t > 0.0f && t_min > t) {
+        t_min = t;
+        hit = g;
+      }
     }
   }
   if (!kd) return false;
@@ -1543,6 +1578,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
       }
       dg[i].wlo[3] = dg[i].whi[3] = 0.0f;
     }
+    if (dg[i].type != 0 && dg[i].type != 1)  // SPHERE / CUBE: the only types the scene parser creates
+      return bail(fail(KDPT_ERR_UNSUPPORTED, "geom type other than sphere (0) or cube (1)"));
     if (dg[i].materialid < 0 || dg[i].materialid >= sc->num_materials)
       return bail(fail(KDPT_ERR_ARG, "geom materialid out of range"));
   }
