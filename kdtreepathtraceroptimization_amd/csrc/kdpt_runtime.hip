@@ -824,9 +824,21 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
 }
 
 // Exclusive scan of the tile counts (one workgroup; <= MAX_KEYS * ntiles entries).
-__global__ __launch_bounds__(1024) void k_scan(const int* __restrict__ tile_counts, int* __restrict__ tile_off,
-                                               const int* counts, int depth, int ntiles_alloc, int nkeys,
-                                               int* total_out) {
+// One workgroup per scan job: job 0 = the survivors (or, when sorting, the per-material histogram),
+// job 1 = the walking survivors of the intersect-stage hand-off (launched only when it runs).
+struct ScanJob {
+  const int* tile_counts;
+  int* tile_off;
+  int nkeys;
+  int* total_out;
+};
+__global__ __launch_bounds__(1024) void k_scan(ScanJob j0, ScanJob j1, const int* counts, int depth,
+                                               int ntiles_alloc) {
+  const ScanJob& J = blockIdx.x == 0 ? j0 : j1;
+  const int* __restrict__ tile_counts = J.tile_counts;
+  int* __restrict__ tile_off = J.tile_off;
+  const int nkeys = J.nkeys;
+  int* total_out = J.total_out;
   const int n = counts[depth];
   const int ntiles = (n + TILE - 1) / TILE;
   const int total_entries = nkeys * ntiles;
@@ -2316,14 +2328,12 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       else launch_shade_h<false>(c, a, compact, sort, st);
       HIP_TRY(hipGetLastError());
       if (compact || sort) {
-        hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, c->tile_counts, c->tile_off, c->counts, depth,
-                           c->ntiles, sort ? c->nkeys : 1, c->counts + depth + 1);
+        // survivors' offsets + the next bounce's path count; with the hand-off also the candidate-list
+        // offsets per tile + the next bounce's candidate count (a second workgroup)
+        const ScanJob j0{c->tile_counts, c->tile_off, sort ? c->nkeys : 1, c->counts + depth + 1};
+        const ScanJob j1{c->tile_ccounts, c->tile_coff, 1, c->ccount + depth + 1};
+        hipLaunchKernelGGL(k_scan, dim3(prep_next ? 2 : 1), dim3(1024), 0, st, j0, j1, c->counts, depth, c->ntiles);
         HIP_TRY(hipGetLastError());
-        if (prep_next) {  // candidate-list offsets per tile and the next bounce's candidate count
-          hipLaunchKernelGGL(k_scan, dim3(1), dim3(1024), 0, st, c->tile_ccounts, c->tile_coff, c->counts, depth,
-                             c->ntiles, 1, c->ccount + depth + 1);
-          HIP_TRY(hipGetLastError());
-        }
         const int nxt = c->cur ^ 1;
         ScatterPrep sp{prep_next ? 1 : 0, c->prep, c->geomhit, c->hits, c->cand, c->tile_coff};
         if (sort)
