@@ -80,7 +80,7 @@ __device__ inline unsigned int lane_prefix(unsigned long long mask) {
 __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int traceDepth, PathBuf out,
                                                   float focalLength, float dofAngle, int antialias, int* counts,
                                                   int ncounts, int* work, int nwork,
-                                                  unsigned long long* trace_t) {
+                                                  unsigned long long* trace_t, unsigned long long* lb, int nlb) {
   const int W = cam.resolution[0], H = cam.resolution[1];
   const int index = blockIdx.x * blockDim.x + threadIdx.x;
   if (index == 0) {
@@ -89,12 +89,14 @@ __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int
     for (int k = 0; k < nwork; k++) {
       work[k] = 0;
       work[nwork + k] = 0;  // candidate counts (k_geoms), stored after the work counters
+      work[2 * nwork + k] = 0;  // k_shade_fused's tile tickets
       trace_t[2 * k] = ~0ull;  // k_trace span of bounce k, then (at 2*nwork) k_geoms' span
       trace_t[2 * k + 1] = 0ull;
       trace_t[2 * nwork + 2 * k] = ~0ull;
       trace_t[2 * nwork + 2 * k + 1] = 0ull;
     }
   }
+  for (int e = index; e < nlb; e += gridDim.x * blockDim.x) lb[e] = 0ull;  // k_shade_fused's look-back records
   if (index >= W * H) return;
   const int x = index % W, y = index / W;
   const f3 view = mk3(cam.view[0], cam.view[1], cam.view[2]);
@@ -708,23 +710,109 @@ struct ShadeArgs {
   Counters* count_aabb;  // count mode: root tests of the rays that end there
 };
 
+// One path's shading (shadeMaterial + scatterRay, src/pathtrace.cu), the partialGather of a path that ends
+// here, and, when the hand-off runs, the next bounce's intersect-stage first part (prep_ray).
+struct ShadeOut {
+  float4 q0, q1, q2;
+  int pm;
+  bool changed, alive, walk, tested;
+  float tm;
+  int gh;
+};
+
+template <bool HYBRID, bool COMPACT>
+__device__ inline void shade_one(const ShadeArgs& A, int i, ShadeOut& o) {
+  const DevScene& S = A.S;
+  const float4 q0 = A.paths.p0[i], q1 = A.paths.p1[i], q2 = A.paths.p2[i];
+  int matHit = A.paths.pm[i];
+  const int pw = fbits(q1.w);
+  const int pix = pw & 0x7fffffff;
+  Ray ray;
+  ray.origin = mk3(q0.x, q0.y, q0.z);
+  ray.direction = mk3(q1.x, q1.y, q1.z);
+  ray.isinside = (pw >> 31) & 1;
+  ray.sdepth = q0.w;
+  f3 color = mk3(q2.x, q2.y, q2.z);
+  int bounces = fbits(q2.w);
+  o.changed = bounces > 0;
+  if (bounces > 0) {
+    const int2 hr = A.hits[i];
+    float isect_t = -1.0f;
+    int isect_mat = 0;
+    if (hr.x != -1) {
+      f3 ip, nrm;
+      float t;
+      int mid;
+      if (hr.x < -1) {  // triangle: the traversal's final recomputation, repeated
+        const int k = -hr.x - 2;
+        float bx, by, bzk;
+        tri_test(S, k, ray.origin, ray.direction, bx, by, bzk);
+        t = tri_hit_t<HYBRID>(S, k, ray.origin, ray.direction, bx, by, bzk, ip, nrm);
+        mid = hr.y;
+      } else {
+        const DevGeom& G = S.geoms[hr.x];
+        t = G.type == 1 ? boxIntersectionTest(G, ray, ip, nrm) : sphereIntersectionTest(G, ray, ip, nrm);
+        mid = G.materialid;
+      }
+      Rng rng = seeded_rng(A.iter, i, A.depth);
+      matHit = mid;
+      scatterRay(ray, ip, nrm, S.materials[mid], rng, A.softness);
+      isect_t = t;
+      isect_mat = mid;
+    }
+    shade(isect_t, isect_mat, S.materials, A.enable_sss != 0, ray, color, bounces);
+  }
+  o.q0 = make_float4(ray.origin.x, ray.origin.y, ray.origin.z, ray.sdepth);
+  o.q1 = make_float4(ray.direction.x, ray.direction.y, ray.direction.z, ibits(pix | ((ray.isinside ? 1 : 0) << 31)));
+  o.q2 = make_float4(color.x, color.y, color.z, ibits(bounces));
+  o.pm = matHit;
+  if (COMPACT && bounces == 0) {
+    // partialGather: one live path per pixel, so this read-modify-write never collides
+    float* px = A.image + 3 * (size_t)pix;
+    px[0] += color.x;
+    px[1] += color.y;
+    px[2] += color.z;
+  }
+  o.alive = COMPACT ? (bounces != 0) : true;
+  o.walk = o.tested = false;
+  o.tm = 0.0f;
+  o.gh = -1;
+  if (COMPACT && A.prep_on && bounces != 0) {
+    o.walk = prep_ray(S, S.has_obj && S.num_nodes > 0, ray.origin, ray.direction, o.tm, o.gh);
+    o.tested = S.has_obj && S.num_nodes > 0;
+  }
+}
+
+__device__ inline void shade_stats(const ShadeArgs& A, int n) {
+  atomicAdd(A.total_segments, (unsigned long long)n);
+  // the intersect kernel of this bounce on the device clock (first block start .. last block end; a
+  // launch that had nothing to do left its record empty)
+  const unsigned long long t0 = A.trace_t[2 * A.depth], t1 = A.trace_t[2 * A.depth + 1];
+  const unsigned long long span = t1 > t0 ? t1 - t0 : 0ull;
+  if (A.trace_total && span) {
+    atomicAdd(&A.trace_total[0], span);
+    atomicAdd(&A.trace_total[1], 1ull);
+  }
+}
+
+__device__ inline void count_prep(const ShadeArgs& A, bool tested, bool walk) {
+  const unsigned long long miss = __ballot(tested && !walk), wm = __ballot(walk);
+  if ((threadIdx.x & 63) == 0 && miss) {
+    atomicAdd(&A.count_aabb->aabb, (unsigned long long)__popcll(miss));
+    atomicAdd(&A.count_aabb->aabb_prep, (unsigned long long)__popcll(miss));
+  }
+  if ((threadIdx.x & 63) == 0 && wm) atomicAdd(&A.count_aabb->cand, (unsigned long long)__popcll(wm));
+}
+
+// Shading in place, then k_scan + k_scatter (the material sort of iteration 2, no compaction, or the
+// trace-order classes).
 template <bool HYBRID, bool COMPACT, bool SORT>
 __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   const int n = A.counts[A.depth];
   const int tile = blockIdx.x;
   if (tile * TILE >= n) return;  // uniform per block
   const int i = tile * TILE + threadIdx.x;
-  if (i == 0) {
-    atomicAdd(A.total_segments, (unsigned long long)n);
-    // the intersect kernel of this bounce on the device clock (first block start .. last block end; a
-    // launch that had nothing to do left its record empty)
-    const unsigned long long t0 = A.trace_t[2 * A.depth], t1 = A.trace_t[2 * A.depth + 1];
-    const unsigned long long span = t1 > t0 ? t1 - t0 : 0ull;
-    if (A.trace_total && span) {
-      atomicAdd(&A.trace_total[0], span);
-      atomicAdd(&A.trace_total[1], 1ull);
-    }
-  }
+  if (i == 0) shade_stats(A, n);
   __shared__ int s_hist[MAX_KEYS];
   __shared__ int s_khist[TRACE_KEYS];
   if (SORT) {
@@ -736,66 +824,21 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   bool alive = false, walk = false, tested = false;
   int key = 0;
   if (i < n) {
-    const float4 q0 = A.paths.p0[i], q1 = A.paths.p1[i], q2 = A.paths.p2[i];
-    int matHit = A.paths.pm[i];
-    const int pw = fbits(q1.w);
-    const int pix = pw & 0x7fffffff;
-    Ray ray;
-    ray.origin = mk3(q0.x, q0.y, q0.z);
-    ray.direction = mk3(q1.x, q1.y, q1.z);
-    ray.isinside = (pw >> 31) & 1;
-    ray.sdepth = q0.w;
-    f3 color = mk3(q2.x, q2.y, q2.z);
-    int bounces = fbits(q2.w);
-    if (bounces > 0) {
-      const int2 hr = A.hits[i];
-      float isect_t = -1.0f;
-      int isect_mat = 0;
-      if (hr.x != -1) {
-        f3 ip, nrm;
-        float t;
-        int mid;
-        if (hr.x < -1) {  // triangle: the traversal's final recomputation, repeated
-          const int k = -hr.x - 2;
-          float bx, by, bzk;
-          tri_test(S, k, ray.origin, ray.direction, bx, by, bzk);
-          t = tri_hit_t<HYBRID>(S, k, ray.origin, ray.direction, bx, by, bzk, ip, nrm);
-          mid = hr.y;
-        } else {
-          const DevGeom& G = S.geoms[hr.x];
-          t = G.type == 1 ? boxIntersectionTest(G, ray, ip, nrm) : sphereIntersectionTest(G, ray, ip, nrm);
-          mid = G.materialid;
-        }
-        Rng rng = seeded_rng(A.iter, i, A.depth);
-        matHit = mid;
-        scatterRay(ray, ip, nrm, S.materials[mid], rng, A.softness);
-        isect_t = t;
-        isect_mat = mid;
-      }
-      shade(isect_t, isect_mat, S.materials, A.enable_sss != 0, ray, color, bounces);
-      A.paths.p0[i] = make_float4(ray.origin.x, ray.origin.y, ray.origin.z, ray.sdepth);
-      A.paths.p1[i] = make_float4(ray.direction.x, ray.direction.y, ray.direction.z,
-                                  ibits(pix | ((ray.isinside ? 1 : 0) << 31)));
-      A.paths.p2[i] = make_float4(color.x, color.y, color.z, ibits(bounces));
-      A.paths.pm[i] = matHit;
+    ShadeOut o;
+    shade_one<HYBRID, COMPACT>(A, i, o);
+    if (o.changed) {
+      A.paths.p0[i] = o.q0;
+      A.paths.p1[i] = o.q1;
+      A.paths.p2[i] = o.q2;
+      A.paths.pm[i] = o.pm;
     }
-    if (COMPACT && bounces == 0) {
-      // partialGather: one live path per pixel, so this read-modify-write never collides
-      float* px = A.image + 3 * (size_t)pix;
-      px[0] += color.x;
-      px[1] += color.y;
-      px[2] += color.z;
-    }
-    alive = COMPACT ? (bounces != 0) : true;
-    key = matHit;
-    if (COMPACT && A.prep_on && bounces != 0) {
-      float tm;
-      int gh;
-      walk = prep_ray(S, S.has_obj && S.num_nodes > 0, ray.origin, ray.direction, tm, gh);
-      tested = S.has_obj && S.num_nodes > 0;
-      A.prep[i] = make_int2(fbits(tm), (gh + 1) | (walk ? 0x10000 : 0));
-    }
-    if (COMPACT && A.tile_kcounts && alive) atomicAdd(&s_khist[trace_class(S, ray.origin, ray.direction)], 1);
+    alive = o.alive;
+    walk = o.walk;
+    tested = o.tested;
+    key = o.pm;
+    if (COMPACT && A.prep_on && alive) A.prep[i] = make_int2(fbits(o.tm), (o.gh + 1) | (walk ? 0x10000 : 0));
+    if (COMPACT && A.tile_kcounts && alive)
+      atomicAdd(&s_khist[trace_class(S, mk3(o.q0.x, o.q0.y, o.q0.z), mk3(o.q1.x, o.q1.y, o.q1.z))], 1);
   }
   if (COMPACT && A.tile_kcounts) {
     __syncthreads();
@@ -812,13 +855,122 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   if (COMPACT && A.prep_on) {
     const int cw = __syncthreads_count(walk);
     if (threadIdx.x == 0) A.tile_ccounts[tile] = cw;
-    if (A.count_aabb) {
-      const unsigned long long miss = __ballot(tested && !walk), wm = __ballot(walk);
-      if ((threadIdx.x & 63) == 0 && miss) {
-        atomicAdd(&A.count_aabb->aabb, (unsigned long long)__popcll(miss));
-        atomicAdd(&A.count_aabb->aabb_prep, (unsigned long long)__popcll(miss));
+    if (A.count_aabb) count_prep(A, tested, walk);
+  }
+}
+
+// Single-pass shading + stable stream compaction (the usual case: compaction on, no material sort).
+// Tiles take tickets in arrival order, publish their survivor / walker counts and find their offsets by a
+// decoupled look-back over the earlier tiles' records (lb: flag << 62 | survivors << 31 | walkers; flag 1 =
+// this tile's counts, 2 = inclusive prefix), then write the survivors straight into the other path buffer in
+// the order the scan + scatter would give, with the next bounce's hand-off records.  A tile writes only
+// after every earlier tile has published, i.e. has read its inputs, and its own slots are >= the ones it
+// writes, so the hit records can be compacted in place.
+struct FuseArgs {
+  PathBuf dst;
+  int* tickets;               // [cap] tile tickets per bounce
+  unsigned long long* lb;     // [cap][ntiles] look-back records
+  int* counts;                // [cap + 2] live paths per bounce
+  int* ccount;                // [cap] candidates per bounce
+  int2* geomhit;
+  int2* hits;
+  int* cand;
+};
+
+__device__ inline unsigned long long lb_load(const unsigned long long* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline void lb_store(unsigned long long* p, unsigned long long v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ inline unsigned long long lb_pack(unsigned long long flag, unsigned s, unsigned w) {
+  return (flag << 62) | ((unsigned long long)s << 31) | (unsigned long long)w;
+}
+
+template <bool HYBRID>
+__global__ __launch_bounds__(TILE) void k_shade_fused(ShadeArgs A, FuseArgs F) {
+  const int n = A.counts[A.depth];
+  __shared__ int s_tile;
+  __shared__ unsigned s_cnt[2][TILE / 64];
+  __shared__ unsigned s_ex[2];
+  if (threadIdx.x == 0) s_tile = atomicAdd(&F.tickets[A.depth], 1);
+  __syncthreads();
+  const int tile = s_tile;
+  if (tile * TILE >= n) return;  // uniform per block
+  const int i = tile * TILE + threadIdx.x;
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  if (i == 0) shade_stats(A, n);
+  ShadeOut o;
+  o.alive = o.walk = o.tested = false;
+  if (i < n) shade_one<HYBRID, true>(A, i, o);
+  const unsigned long long ms = __ballot(o.alive), mw = __ballot(o.walk);
+  if (A.count_aabb && A.prep_on) count_prep(A, o.tested, o.walk);
+  if (lane == 0) {
+    s_cnt[0][wid] = (unsigned)__popcll(ms);
+    s_cnt[1][wid] = (unsigned)__popcll(mw);
+  }
+  __syncthreads();
+  if (wid == 0) {
+    unsigned aS = 0, aW = 0;
+    for (int w = 0; w < TILE / 64; w++) {
+      aS += s_cnt[0][w];
+      aW += s_cnt[1][w];
+    }
+    unsigned long long* lb = F.lb + (size_t)A.depth * A.ntiles;
+    unsigned eS = 0, eW = 0;
+    if (tile == 0) {
+      if (lane == 0) lb_store(lb, lb_pack(2, aS, aW));
+    } else {
+      if (lane == 0) lb_store(lb + tile, lb_pack(1, aS, aW));
+      for (int base = tile - 1;; base -= 64) {
+        const int j = base - lane;
+        unsigned long long v = j >= 0 ? lb_load(lb + j) : lb_pack(2, 0, 0);
+        while (__ballot((v >> 62) == 0)) {
+          __builtin_amdgcn_s_sleep(1);
+          if ((v >> 62) == 0) v = lb_load(lb + j);
+        }
+        const unsigned long long pre = __ballot((v >> 62) == 2);
+        const int upto = pre ? __ffsll((long long)pre) - 1 : 63;  // nearest inclusive prefix, and the counts before it
+        unsigned s = lane <= upto ? (unsigned)(v >> 31) & 0x7fffffffu : 0u;
+        unsigned w = lane <= upto ? (unsigned)v & 0x7fffffffu : 0u;
+        for (int off = 32; off > 0; off >>= 1) {
+          s += __shfl_xor(s, off);
+          w += __shfl_xor(w, off);
+        }
+        eS += s;
+        eW += w;
+        if (pre) break;
       }
-      if ((threadIdx.x & 63) == 0 && wm) atomicAdd(&A.count_aabb->cand, (unsigned long long)__popcll(wm));
+      if (lane == 0) lb_store(lb + tile, lb_pack(2, eS + aS, eW + aW));
+    }
+    if (lane == 0) {
+      s_ex[0] = eS;
+      s_ex[1] = eW;
+      if (tile == (n - 1) / TILE) {  // the last tile: the next bounce's path and candidate counts
+        F.counts[A.depth + 1] = (int)(eS + aS);
+        if (A.prep_on) F.ccount[A.depth + 1] = (int)(eW + aW);
+      }
+    }
+  }
+  __syncthreads();
+  if (o.alive) {
+    unsigned bS = s_ex[0], bW = s_ex[1];
+    for (int w = 0; w < wid; w++) {
+      bS += s_cnt[0][w];
+      bW += s_cnt[1][w];
+    }
+    const int d = (int)(bS + lane_prefix(ms));
+    F.dst.p0[d] = o.q0;
+    F.dst.p1[d] = o.q1;
+    F.dst.p2[d] = o.q2;
+    F.dst.pm[d] = o.pm;
+    if (A.prep_on) {
+      if (o.walk) {
+        F.geomhit[d] = make_int2(fbits(o.tm), o.gh);
+        F.cand[bW + lane_prefix(mw)] = d;
+      } else {
+        F.hits[d] = make_int2(o.gh, -1);  // final: the analytic geoms' hit (code -1: none)
+      }
     }
   }
 }
@@ -1072,6 +1224,8 @@ struct kdpt_ctx {
   int* tile_ccounts = nullptr;  // [ntiles] walking survivors per tile, and their offsets
   int* tile_coff = nullptr;
   int* ccount = nullptr;    // [cap] their number per bounce (inside the counts allocation)
+  int* tickets = nullptr;   // [cap] k_shade_fused's tile tickets (inside the counts allocation)
+  unsigned long long* lb = nullptr;  // [cap][ntiles] k_shade_fused's look-back records
   int tree_mode = 0;      // TreeMode
   int trace_grid = 0;     // persistent intersect workgroups
   bool grid_env = false;  // trace_grid fixed by KDPT_TRACE_GRID_FRAC
@@ -1082,6 +1236,7 @@ struct kdpt_ctx {
   int* tile_koff = nullptr;
   int* perm = nullptr;          // trace order of the next bounce
   bool trace_order = true;      // KDPT_TRACE_ORDER=0 disables (identity order)
+  bool no_fuse = false;         // KDPT_SHADE_FUSED=0: k_shade + k_scan + k_scatter instead of k_shade_fused
   int chunk_width[3] = {16, 64, 64};
   Counters* counters = nullptr;
   Counters last_profile{};
@@ -1172,7 +1327,7 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
   // counts[cap+3 ..]: work counters of the persistent intersect kernel
   if ((rc = dalloc(c, &c->trace_t, 4 * (size_t)c->cap))) return rc;
   HIP_TRY(hipMemset(c->trace_t, 0, sizeof(unsigned long long) * 4 * c->cap));
-  if ((rc = dalloc(c, &c->counts, 3 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
+  if ((rc = dalloc(c, &c->counts, 4 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->lb, (size_t)c->cap * c->ntiles)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->cand, (size_t)c->npix)) || (rc = dalloc(c, &c->prep, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->tile_ccounts, (size_t)c->ntiles)) || (rc = dalloc(c, &c->tile_coff, (size_t)c->ntiles)) ||
       (rc = dalloc(c, &c->geomhit, (size_t)c->npix)) ||
@@ -1184,10 +1339,12 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
     return rc;
   if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 3), hipHostMallocDefault) != hipSuccess)
     return fail(KDPT_ERR_HIP, "hipHostMalloc");
-  HIP_TRY(hipMemset(c->counts, 0, sizeof(int) * (3 * c->cap + 3)));
+  HIP_TRY(hipMemset(c->counts, 0, sizeof(int) * (4 * c->cap + 3)));
+  HIP_TRY(hipMemset(c->lb, 0, sizeof(unsigned long long) * c->cap * c->ntiles));
   c->S.fault = c->counts + c->cap + 2;
   c->work = c->counts + c->cap + 3;
   c->ccount = c->work + c->cap;
+  c->tickets = c->ccount + c->cap;
   return KDPT_OK;
 }
 
@@ -1220,6 +1377,7 @@ int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
   c->trace_grid = p->trace_grid;
   c->tree_lds = p->tree_lds;
   c->trace_order = p->trace_order;
+  c->no_fuse = p->no_fuse;
   for (int k = 0; k < 3; k++) c->chunk_width[k] = p->chunk_width[k];
   c->counters = p->counters;
   c->total_segments = p->total_segments;
@@ -1760,6 +1918,7 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     if (cw) sscanf(cw, "%d,%d,%d", &c->chunk_width[0], &c->chunk_width[1], &c->chunk_width[2]);
     for (int k = 0; k < 3; k++) c->chunk_width[k] = std::min(64, std::max(1, c->chunk_width[k]));
     c->trace_order = false;  // superseded by k_geoms' candidate lists (KDPT_TRACE_ORDER is ignored)
+    if (const char* f = getenv("KDPT_SHADE_FUSED")) c->no_fuse = f[0] == '0';
   }
   if ((rc = setup_trace(c))) return bail(rc);
   c->S.trip_limit = 8 * std::max(c->S.num_nodes, 1) + 64;
@@ -2217,7 +2376,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     c->cur = 0;
     hipLaunchKernelGGL(k_gen_rays, dim3((c->npix + 255) / 256), dim3(256), 0, st, c->cam, gen_iter, c->traceDepth,
                        c->buf[0], c->opt.focal_length, c->opt.dof_angle, c->opt.antialias, c->counts, c->cap + 2,
-                       c->work, c->cap, c->trace_t);
+                       c->work, c->cap, c->trace_t, c->lb, c->cap * c->ntiles);
     HIP_TRY(hipGetLastError());
   }
   const bool compact = c0->opt.compaction != 0;
@@ -2323,6 +2482,18 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       a.prep = c->prep;
       a.tile_ccounts = c->tile_ccounts;
       a.count_aabb = count ? c0->counters : nullptr;
+      if (compact && !sort && !a.tile_kcounts && !c->no_fuse) {
+        // single pass: shading, compaction into the other buffer and the hand-off (k_shade_fused)
+        const int nxt = c->cur ^ 1;
+        const FuseArgs f{c->buf[nxt], c->tickets, c->lb, c->counts, c->ccount, c->geomhit, c->hits, c->cand};
+        if (c->opt.short_stack || c->brute)
+          hipLaunchKernelGGL(k_shade_fused<true>, dim3(c->ntiles), dim3(TILE), 0, st, a, f);
+        else
+          hipLaunchKernelGGL(k_shade_fused<false>, dim3(c->ntiles), dim3(TILE), 0, st, a, f);
+        HIP_TRY(hipGetLastError());
+        c->cur = nxt;
+        continue;
+      }
       // hit point offset: 1e-4 for the hybrid traversal and the brute-force kernel, 1e-5 for traverseKDbare
       if (c->opt.short_stack || c->brute) launch_shade_h<true>(c, a, compact, sort, st);
       else launch_shade_h<false>(c, a, compact, sort, st);

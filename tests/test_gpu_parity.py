@@ -127,6 +127,29 @@ def test_path_state_after_each_bounce(kdpt, oracle, stop_depth):
         assert np.array_equal(g[f], o[f]), f
 
 
+@pytest.mark.parametrize("res", [(96, 96), (800, 800)])
+def test_fused_shading_equals_scan_scatter(kdpt, oracle, monkeypatch, res):
+    """k_shade_fused (single-pass decoupled look-back compaction) and k_shade + k_scan + k_scatter
+    (KDPT_SHADE_FUSED=0) give the same images and path arrays; the small size also against the oracle.
+    800x800 has 2500 tiles per bounce, so most tiles find their offset through other tiles' counts."""
+    desc = load_fixture_scene("cornell", "dragon_5", res=res, depth=8)
+    out = {}
+    for fused in ("1", "0"):
+        monkeypatch.setenv("KDPT_SHADE_FUSED", fused)
+        with _pt(kdpt, desc) as pt:
+            paths = pt.debug_paths(3, 2)
+            pt.reset()
+            for it in (1, 3, 4):
+                pt.trace_iteration(it)
+            out[fused] = (paths, pt.image().copy())
+    for f in ("origin", "direction", "color", "pixelIndex", "remainingBounces", "materialIdHit", "isinside"):
+        assert np.array_equal(out["1"][0][f], out["0"][0][f]), f
+    assert np.array_equal(out["1"][1].view(np.uint32), out["0"][1].view(np.uint32))
+    if res == (96, 96):
+        o = oracle.OracleScene.from_description(desc).paths_after(3, 2)
+        assert np.array_equal(out["1"][0]["pixelIndex"], o["pixelIndex"])
+
+
 def test_iteration2_sort_order(kdpt, oracle):
     """Iteration 2 stable-sorts the live paths by materialIdHit after compaction (src/pathtrace.cu:2600-2606)."""
     desc = load_fixture_scene("cornell", "sphere_low_1", res=(80, 80), depth=8)
