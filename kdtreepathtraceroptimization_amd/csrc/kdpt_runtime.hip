@@ -721,8 +721,7 @@ struct ShadeOut {
 };
 
 template <bool HYBRID, bool COMPACT>
-__device__ inline void shade_one(const ShadeArgs& A, int i, ShadeOut& o) {
-  const DevScene& S = A.S;
+__device__ inline void shade_one(const ShadeArgs& A, const DevScene& S, int i, ShadeOut& o) {
   const float4 q0 = A.paths.p0[i], q1 = A.paths.p1[i], q2 = A.paths.p2[i];
   int matHit = A.paths.pm[i];
   const int pw = fbits(q1.w);
@@ -825,7 +824,7 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   int key = 0;
   if (i < n) {
     ShadeOut o;
-    shade_one<HYBRID, COMPACT>(A, i, o);
+    shade_one<HYBRID, COMPACT>(A, A.S, i, o);
     if (o.changed) {
       A.paths.p0[i] = o.q0;
       A.paths.p1[i] = o.q1;
@@ -887,22 +886,38 @@ __device__ inline unsigned long long lb_pack(unsigned long long flag, unsigned s
   return (flag << 62) | ((unsigned long long)s << 31) | (unsigned long long)w;
 }
 
-template <bool HYBRID>
+// STAGE: the analytic geoms and the materials copied into LDS first (small scenes: their per-lane reads,
+// indexed by hit and by nearest-first order, are then LDS reads instead of L2 round trips)
+constexpr int STAGE_MATS = 32;
+template <bool HYBRID, bool STAGE>
 __global__ __launch_bounds__(TILE) void k_shade_fused(ShadeArgs A, FuseArgs F) {
   const int n = A.counts[A.depth];
   __shared__ int s_tile;
   __shared__ unsigned s_cnt[2][TILE / 64];
   __shared__ unsigned s_ex[2];
+  static_assert(sizeof(DevGeom) % 4 == 0 && sizeof(DevMaterial) % 4 == 0, "staged as dwords");
+  __shared__ uint32_t s_geoms[STAGE ? ORDERED_GEOMS * sizeof(DevGeom) / 4 : 1];
+  __shared__ uint32_t s_mats[STAGE ? STAGE_MATS * sizeof(DevMaterial) / 4 : 1];
   if (threadIdx.x == 0) s_tile = atomicAdd(&F.tickets[A.depth], 1);
+  if (STAGE) {
+    const int gw = A.S.num_geoms * (int)(sizeof(DevGeom) / 4), mw = A.S.num_materials * (int)(sizeof(DevMaterial) / 4);
+    for (int k = threadIdx.x; k < gw; k += TILE) s_geoms[k] = reinterpret_cast<const uint32_t*>(A.S.geoms)[k];
+    for (int k = threadIdx.x; k < mw; k += TILE) s_mats[k] = reinterpret_cast<const uint32_t*>(A.S.materials)[k];
+  }
   __syncthreads();
   const int tile = s_tile;
   if (tile * TILE >= n) return;  // uniform per block
+  DevScene S = A.S;
+  if (STAGE) {
+    S.geoms = reinterpret_cast<const DevGeom*>(s_geoms);
+    S.materials = reinterpret_cast<const DevMaterial*>(s_mats);
+  }
   const int i = tile * TILE + threadIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (i == 0) shade_stats(A, n);
   ShadeOut o;
   o.alive = o.walk = o.tested = false;
-  if (i < n) shade_one<HYBRID, true>(A, i, o);
+  if (i < n) shade_one<HYBRID, true>(A, S, i, o);
   const unsigned long long ms = __ballot(o.alive), mw = __ballot(o.walk);
   if (A.count_aabb && A.prep_on) count_prep(A, o.tested, o.walk);
   if (lane == 0) {
@@ -2486,10 +2501,12 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         // single pass: shading, compaction into the other buffer and the hand-off (k_shade_fused)
         const int nxt = c->cur ^ 1;
         const FuseArgs f{c->buf[nxt], c->tickets, c->lb, c->counts, c->ccount, c->geomhit, c->hits, c->cand};
-        if (c->opt.short_stack || c->brute)
-          hipLaunchKernelGGL(k_shade_fused<true>, dim3(c->ntiles), dim3(TILE), 0, st, a, f);
-        else
-          hipLaunchKernelGGL(k_shade_fused<false>, dim3(c->ntiles), dim3(TILE), 0, st, a, f);
+        const bool stage = c->S.num_geoms + c->S.num_boxes <= ORDERED_GEOMS && c->S.num_materials <= STAGE_MATS;
+        const bool hyb = c->opt.short_stack || c->brute;
+        if (hyb && stage) hipLaunchKernelGGL((k_shade_fused<true, true>), dim3(c->ntiles), dim3(TILE), 0, st, a, f);
+        else if (hyb) hipLaunchKernelGGL((k_shade_fused<true, false>), dim3(c->ntiles), dim3(TILE), 0, st, a, f);
+        else if (stage) hipLaunchKernelGGL((k_shade_fused<false, true>), dim3(c->ntiles), dim3(TILE), 0, st, a, f);
+        else hipLaunchKernelGGL((k_shade_fused<false, false>), dim3(c->ntiles), dim3(TILE), 0, st, a, f);
         HIP_TRY(hipGetLastError());
         c->cur = nxt;
         continue;
