@@ -500,27 +500,43 @@ __device__ inline float readlane_f(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
 }
 
+// Whole-wave reductions on DPP lane moves (VALU only; HIP's __shfl_* are ds_bpermute, an LDS round trip per
+// step).  quad_perm xor 1 and xor 2, then the half-row and row mirrors give every lane its 16-lane row's
+// result; row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry the lower rows into row 3, so lane 63
+// ends with the whole wave's, read into a scalar register.  Every lane of the wave must be active.
+template <int CTRL, int ROWS>
+__device__ inline uint32_t dpp_u32(uint32_t v) {
+  return (uint32_t)__builtin_amdgcn_update_dpp((int)v, (int)v, CTRL, ROWS, 0xF, false);
+}
+template <int CTRL, int ROWS>
+__device__ inline unsigned long long dpp_u64(unsigned long long v) {
+  return ((unsigned long long)dpp_u32<CTRL, ROWS>((uint32_t)(v >> 32)) << 32) | dpp_u32<CTRL, ROWS>((uint32_t)v);
+}
+__device__ inline unsigned long long lane63_u64(unsigned long long v) {
+  return ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
+}
+#define KDPT_WAVE_REDUCE(STEP) STEP(0xB1, 0xF) STEP(0x4E, 0xF) STEP(0x141, 0xF) STEP(0x140, 0xF) \
+                               STEP(0x142, 0xA) STEP(0x143, 0xC)
+
 __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const unsigned long long o = __shfl_xor(v, off);
-    v = o < v ? o : v;
-  }
-  return v;
+#define KDPT_STEP(C, R) { const unsigned long long o = dpp_u64<C, R>(v); v = o < v ? o : v; }
+  KDPT_WAVE_REDUCE(KDPT_STEP)
+#undef KDPT_STEP
+  return lane63_u64(v);
 }
 
 __device__ inline unsigned long long wave_max_u64(unsigned long long v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const unsigned long long o = __shfl_xor(v, off);
-    v = o > v ? o : v;
-  }
-  return v;
+#define KDPT_STEP(C, R) { const unsigned long long o = dpp_u64<C, R>(v); v = o > v ? o : v; }
+  KDPT_WAVE_REDUCE(KDPT_STEP)
+#undef KDPT_STEP
+  return lane63_u64(v);
 }
 __device__ inline int wave_max_i32(int v) {
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) v = max(v, __shfl_xor(v, off));
-  return v;
+#define KDPT_STEP(C, R) v = max(v, (int)dpp_u32<C, R>((uint32_t)v));
+  KDPT_WAVE_REDUCE(KDPT_STEP)
+#undef KDPT_STEP
+  return __builtin_amdgcn_readlane(v, 63);
 }
 
 // May the LINE through o (both directions: glm's u/v tests ignore the sign of t) cross the cluster's
