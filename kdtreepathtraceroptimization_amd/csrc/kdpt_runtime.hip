@@ -16,6 +16,8 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <cfloat>
+#include <cmath>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -487,6 +489,8 @@ struct BruteArgs {
   int2* hits;
   const BruteShape* shapes;
   int num_shapes;
+  const float4* chunk_lo;  // boxes of the file-order triangles [64j, 64j + 64) (the tested triangles
+  const float4* chunk_hi;  // v0, v0 + e1, v0 + e2, rounded outward)
   Counters* counters;
   unsigned long long* trace_t;
 };
@@ -581,6 +585,8 @@ __global__ __launch_bounds__(TILE) void k_brute(BruteArgs A) {
     }
   }
   // the polygon loop (src/pathtrace.cu:485-576)
+  const f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+  const bool cull = __all(!live || (fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV));
   TraverseCounters cnt{};
   int best = -1;
   int objMat = -1;
@@ -599,9 +605,19 @@ __global__ __launch_bounds__(TILE) void k_brute(BruteArgs A) {
           // every lane that tests this shape starts at the same triangle: scalar triangle fetches
           const int k0 = __builtin_amdgcn_readfirstlane(it0 / 3);
           const int nt = nidx / 3;
-          for (int k = k0; k < k0 + nt; k++) {
-            const TriData T = tri_load(S, k);
-            brute_triangle<COUNT>(S, k, T, o, d, t_min, best, take, cnt);
+          // 64-triangle chunks: no triangle of a chunk whose box the lane's line misses (box widened as in
+          // cluster_may_pass) passes the u/v tests, so those lanes skip it, and the wave skips a chunk no lane
+          // can hit; the others test its triangles in file order as before
+          for (int k = k0; k < k0 + nt;) {
+            const int j = k >> 6, kend = min(k0 + nt, (j + 1) << 6);
+            const bool may = take && (!cull || cluster_may_pass(A.chunk_lo[j], A.chunk_hi[j], o, inv));
+            if (__any(may)) {
+              for (; k < kend; k++) {
+                const TriData T = tri_load(S, k);
+                brute_triangle<COUNT>(S, k, T, o, d, t_min, best, may, cnt);
+              }
+            }
+            k = kend;
           }
         } else {
           const int nt = nidx / 3;
@@ -1285,6 +1301,8 @@ struct kdpt_ctx {
   bool viz = false;  // viz_kd: the KD node boxes drawn as boxes (k_viz)
   BruteShape* shapes = nullptr;
   int num_shapes = 0;
+  float4* chunk_lo = nullptr;  // brute force: boxes of 64 file-order triangles
+  float4* chunk_hi = nullptr;
 };
 
 namespace {
@@ -1403,6 +1421,8 @@ int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
   c->viz = p->viz;
   c->shapes = p->shapes;
   c->num_shapes = p->num_shapes;
+  c->chunk_lo = p->chunk_lo;
+  c->chunk_hi = p->chunk_hi;
   int rc;
   if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     kdpt_destroy(c);
@@ -1874,6 +1894,29 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
       n1[k] = make_float4(nb[0], nb[1], nb[2], 0.0f);
       n2[k] = make_float4(nc[0], nc[1], nc[2], 0.0f);
     }
+    const int nch = std::max(1, (nt + 63) / 64);
+    std::vector<float4> clo(nch), chi(nch);
+    for (int j = 0; j < nch; j++) {
+      double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+      for (int k = 64 * j; k < std::min(nt, 64 * j + 64); k++) {
+        const double v[3] = {tv[k].x, tv[k].y, tv[k].z}, a[3] = {e1[k].x, e1[k].y, e1[k].z},
+                     b[3] = {e2[k].x, e2[k].y, e2[k].z};
+        for (int r = 0; r < 3; r++) {  // the triangle glm tests: v0 + u e1 + v e2, exact in double
+          lo[r] = std::min({lo[r], v[r], v[r] + a[r], v[r] + b[r]});
+          hi[r] = std::max({hi[r], v[r], v[r] + a[r], v[r] + b[r]});
+        }
+      }
+      float l[3], h[3];
+      for (int r = 0; r < 3; r++) {
+        if (lo[r] > hi[r]) lo[r] = hi[r] = 0.0;  // empty chunk (no triangles)
+        l[r] = (float)lo[r];
+        if ((double)l[r] > lo[r]) l[r] = std::nextafter(l[r], -FLT_MAX);
+        h[r] = (float)hi[r];
+        if ((double)h[r] < hi[r]) h[r] = std::nextafter(h[r], FLT_MAX);
+      }
+      clo[j] = make_float4(l[0], l[1], l[2], 0.0f);
+      chi[j] = make_float4(h[0], h[1], h[2], 0.0f);
+    }
     std::vector<BruteShape> shp(sc->num_shapes);
     for (int i = 0; i < sc->num_shapes; i++) {
       // glm::vec3(obj_polysbboxes[i] - 0.01, ...): double arithmetic, rounded to float by the constructor
@@ -1891,7 +1934,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     if ((rc = dupload(c, &dtv, tv.data(), nt)) || (rc = dupload(c, &de1, e1.data(), nt)) ||
         (rc = dupload(c, &de2, e2.data(), nt)) || (rc = dupload(c, &dn0, n0.data(), nt)) ||
         (rc = dupload(c, &dn1, n1.data(), nt)) || (rc = dupload(c, &dn2, n2.data(), nt)) ||
-        (rc = dupload(c, &c->shapes, shp.data(), shp.size())))
+        (rc = dupload(c, &c->shapes, shp.data(), shp.size())) ||
+        (rc = dupload(c, &c->chunk_lo, clo.data(), clo.size())) || (rc = dupload(c, &c->chunk_hi, chi.data(), chi.size())))
       return bail(rc);
     c->S.tv0 = dtv;
     c->S.te1 = de1;
@@ -2432,6 +2476,8 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         ba.hits = c->hits;
         ba.shapes = c->shapes;
         ba.num_shapes = c->num_shapes;
+        ba.chunk_lo = c->chunk_lo;
+        ba.chunk_hi = c->chunk_hi;
         ba.counters = c0->counters;
         ba.trace_t = c0->trace_t;
         const dim3 g(c->ntiles), bl(TILE);
