@@ -63,16 +63,18 @@ def parse():
     return ap.parse_args()
 
 
-def cpu_baseline(args):
+def cpu_baseline(args, threads=None, seconds=None):
     """The oracle (plain-C port of the reference path) on this host's cores, bounded sample."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     from kdtreepathtraceroptimization_amd.fixtures import load_fixture_scene
-    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    if threads is None:
+        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+    seconds = args.cpu_seconds if seconds is None else seconds
     s = oracle_lib.OracleScene.from_description(
         load_fixture_scene(args.scene, args.mesh, res=tuple(args.res), depth=args.depth))
     seg, t, it = 0, 0.0, 3
-    while t < args.cpu_seconds and it < 3 + 64:
+    while t < seconds and it < 3 + 64:
         t0 = time.perf_counter()
         _, st = s.render(it, 1, nthreads=threads, shortstack=0 if args.bare else 1, bounce_cap=args.bounce_cap)
         t += time.perf_counter() - t0
@@ -222,6 +224,8 @@ def main():
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
+        # SURVEY 8(d) / BASELINE.md 3: the same oracle on one core as well (at least one whole iteration)
+        out["cpu_baseline_1core"] = cpu_baseline(args, threads=1, seconds=args.cpu_seconds / 2)
     pt.close()
     if dist:
         dist.destroy_process_group()
