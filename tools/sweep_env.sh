@@ -4,7 +4,7 @@
 VAR=$1; VALS=$2; shift 2
 mkdir -p gpurun_out
 for v in $VALS; do
-  env "$VAR=$v" timeout -k 10 120 python -u bench.py --no-cpu-baseline --steps 12 --warmup 2 "$@" > gpurun_out/sweep.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/sweep.log; exit 1; }
+  env "$VAR=$v" timeout -k 10 120 python -u bench.py --no-cpu-baseline --steps 96 --warmup 8 "$@" > gpurun_out/sweep.log 2>&1 || { echo "$v failed"; tail -3 gpurun_out/sweep.log; exit 1; }
   python -c "
 import json; d=json.loads(open('gpurun_out/sweep.log').read().strip().splitlines()[-1])
 print('$VAR=$v', d['value'], d['ms_per_step'], d['roofline']['avg_launch_ms'])"
