@@ -915,14 +915,17 @@ __global__ __launch_bounds__(TILE) void k_shade_fused(ShadeArgs A, FuseArgs F) {
   __shared__ uint32_t s_geoms[STAGE ? ORDERED_GEOMS * sizeof(DevGeom) / 4 : 1];
   __shared__ uint32_t s_mats[STAGE ? STAGE_MATS * sizeof(DevMaterial) / 4 : 1];
   if (threadIdx.x == 0) s_tile = atomicAdd(&F.tickets[A.depth], 1);
+  __syncthreads();
+  const int tile = s_tile;
+  // uniform per block; the grid covers every pixel, so past the first bounces most blocks leave here,
+  // before staging anything
+  if (tile * TILE >= n) return;
   if (STAGE) {
     const int gw = A.S.num_geoms * (int)(sizeof(DevGeom) / 4), mw = A.S.num_materials * (int)(sizeof(DevMaterial) / 4);
     for (int k = threadIdx.x; k < gw; k += TILE) s_geoms[k] = reinterpret_cast<const uint32_t*>(A.S.geoms)[k];
     for (int k = threadIdx.x; k < mw; k += TILE) s_mats[k] = reinterpret_cast<const uint32_t*>(A.S.materials)[k];
+    __syncthreads();
   }
-  __syncthreads();
-  const int tile = s_tile;
-  if (tile * TILE >= n) return;  // uniform per block
   DevScene S = A.S;
   if (STAGE) {
     S.geoms = reinterpret_cast<const DevGeom*>(s_geoms);
