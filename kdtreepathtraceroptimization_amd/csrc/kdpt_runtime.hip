@@ -82,7 +82,8 @@ __device__ inline unsigned int lane_prefix(unsigned long long mask) {
 __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int traceDepth, PathBuf out,
                                                   float focalLength, float dofAngle, int antialias, int* counts,
                                                   int ncounts, int* work, int nwork,
-                                                  unsigned long long* trace_t, unsigned long long* lb, int nlb) {
+                                                  unsigned long long* trace_t, unsigned long long* lb, int nlb,
+                                                  float* zero_image) {
   const int W = cam.resolution[0], H = cam.resolution[1];
   const int index = blockIdx.x * blockDim.x + threadIdx.x;
   if (index == 0) {
@@ -100,6 +101,11 @@ __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int
   }
   for (int e = index; e < nlb; e += gridDim.x * blockDim.x) lb[e] = 0ull;  // k_shade_fused's look-back records
   if (index >= W * H) return;
+  if (zero_image) {  // batched iterations: this iteration's partial image starts at zero (no separate fill)
+    zero_image[3 * index] = 0.0f;
+    zero_image[3 * index + 1] = 0.0f;
+    zero_image[3 * index + 2] = 0.0f;
+  }
   const int x = index % W, y = index / W;
   const f3 view = mk3(cam.view[0], cam.view[1], cam.view[2]);
   const f3 right = mk3(cam.right[0], cam.right[1], cam.right[2]);
@@ -1271,6 +1277,7 @@ struct kdpt_ctx {
   int* perm = nullptr;          // trace order of the next bounce
   bool trace_order = true;      // KDPT_TRACE_ORDER=0 disables (identity order)
   bool no_fuse = false;         // KDPT_SHADE_FUSED=0: k_shade + k_scan + k_scatter instead of k_shade_fused
+  bool zero_partial = false;    // k_gen_rays zeroes `image` (a pipeline slot's per-iteration partial image)
   int chunk_width[3] = {16, 64, 64};
   Counters* counters = nullptr;
   Counters last_profile{};
@@ -2123,7 +2130,7 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
     int iters[MAXB];
     for (int b = 0; b < nb; b++) {
       iters[b] = first_iter + (kb + b) * stride;
-      HIP_TRY(hipMemsetAsync(grp[b]->image, 0, sizeof(float) * 3 * (size_t)c->npix, st));
+      grp[b]->zero_partial = true;  // k_gen_rays clears the partial image (after slot_free, on st)
     }
     std::vector<hipEvent_t>* bev = nullptr;
     if (c->opt.testing_mode) {
@@ -2440,7 +2447,8 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     c->cur = 0;
     hipLaunchKernelGGL(k_gen_rays, dim3((c->npix + 255) / 256), dim3(256), 0, st, c->cam, gen_iter, c->traceDepth,
                        c->buf[0], c->opt.focal_length, c->opt.dof_angle, c->opt.antialias, c->counts, c->cap + 2,
-                       c->work, c->cap, c->trace_t, c->lb, c->cap * c->ntiles);
+                       c->work, c->cap, c->trace_t, c->lb, c->cap * c->ntiles,
+                       c->zero_partial ? c->image : nullptr);
     HIP_TRY(hipGetLastError());
   }
   const bool compact = c0->opt.compaction != 0;
