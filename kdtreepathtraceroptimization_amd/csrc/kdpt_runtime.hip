@@ -1447,9 +1447,18 @@ int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
   return KDPT_OK;
 }
 
-__global__ void k_accumulate(float* __restrict__ image, const float* __restrict__ part, int n3) {
+// A batch's partial images added in iteration order (one add per pixel and iteration, as partialGather
+// does), with one read and one write of the accumulation image per batch instead of one per iteration.
+struct PartialImages {
+  const float* p[MAXB];
+  int nb;
+};
+__global__ void k_accumulate_batch(float* __restrict__ image, PartialImages parts, int n3) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
-  if (i < n3) image[i] += part[i];  // one add per pixel and iteration, as partialGather does
+  if (i >= n3) return;
+  float v = image[i];
+  for (int b = 0; b < parts.nb; b++) v += parts.p[b][i];
+  image[i] = v;
 }
 
 // Read back the intersect-kernel events of finished iterations (testing_mode).
@@ -2149,11 +2158,12 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
     HIP_TRY(hipEventRecord(c->slot_done[g], st));
     HIP_TRY(hipStreamWaitEvent(c->accum_stream, c->slot_done[g], 0));
     const int n3 = 3 * c->npix;
-    for (int b = 0; b < nb; b++) {  // in iteration order
-      hipLaunchKernelGGL(k_accumulate, dim3((n3 + 255) / 256), dim3(256), 0, c->accum_stream, c->image,
-                         grp[b]->image, n3);
-      HIP_TRY(hipGetLastError());
-    }
+    PartialImages parts{};
+    parts.nb = nb;
+    for (int b = 0; b < nb; b++) parts.p[b] = grp[b]->image;  // in iteration order
+    hipLaunchKernelGGL(k_accumulate_batch, dim3((n3 + 255) / 256), dim3(256), 0, c->accum_stream, c->image, parts,
+                       n3);
+    HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->slot_free[g], c->accum_stream));
   }
   HIP_TRY(hipEventDestroy(entry));
