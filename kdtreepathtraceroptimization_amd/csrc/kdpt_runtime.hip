@@ -746,6 +746,9 @@ template <bool HYBRID, bool COMPACT>
 __device__ inline void shade_one(const ShadeArgs& A, const DevScene& S, int i, ShadeOut& o) {
   const float4 q0 = A.paths.p0[i], q1 = A.paths.p1[i], q2 = A.paths.p2[i];
   int matHit = A.paths.pm[i];
+  // issued with the path loads (every listed slot has a record; unused when the path has no bounces
+  // left), not after the bounce test: one dependent HBM round trip less per path
+  const int2 hr = A.hits[i];
   const int pw = fbits(q1.w);
   const int pix = pw & 0x7fffffff;
   Ray ray;
@@ -757,7 +760,6 @@ __device__ inline void shade_one(const ShadeArgs& A, const DevScene& S, int i, S
   int bounces = fbits(q2.w);
   o.changed = bounces > 0;
   if (bounces > 0) {
-    const int2 hr = A.hits[i];
     float isect_t = -1.0f;
     int isect_mat = 0;
     if (hr.x != -1) {
