@@ -60,6 +60,9 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=8,
                     help="batches in flight (kdpt_trace_iterations; bit-identical to one at a time)")
     ap.add_argument("--batch", type=int, default=4, help="iterations sharing each intersect launch (<= 4)")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="nccl = RCCL over xGMI (one GPU per rank); gloo = host-side reduce, for rehearsing the "
+                         "N > 1 path with several ranks sharing one GPU")
     return ap.parse_args()
 
 
@@ -92,12 +95,15 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     import torch
     dist = None
+    ndev = max(1, torch.cuda.device_count())
+    local = local % ndev if args.dist_backend == "gloo" else local  # gloo rehearsal: ranks may share a GPU
+    torch.cuda.set_device(local)
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
-    else:
-        torch.cuda.set_device(local)
+        if args.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group("gloo")
     from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options, load_fixture_scene
 
     desc = load_fixture_scene(args.scene, args.mesh, res=tuple(args.res), depth=args.depth)
@@ -148,7 +154,7 @@ def main():
     launches = st1.intersect_device_launches_total - st0.intersect_device_launches_total
     if dist:
         t = torch.tensor([dt, float(seg), kernel_ms, float(launches), ev_ms, float(ev_launches)], dtype=torch.float64,
-                         device=f"cuda:{local}")
+                         device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
         tmax = t[0:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t[1:].clone()
@@ -195,7 +201,9 @@ def main():
                    "scene": args.scene, "mesh": args.mesh, "resolution": [W, H], "depth": args.depth,
                    "bounce_cap": args.bounce_cap,
                    "kd_nodes": sd.view.num_nodes, "kd_tri_refs": sd.view.num_tris,
-                   "parallelism": f"spp-sharded x{world} + RCCL reduce" if world > 1 else "single GPU"},
+                   "parallelism": (f"spp-sharded x{world} + " + ("RCCL reduce" if args.dist_backend == "nccl" else
+                                                                 "gloo host reduce (ranks sharing GPUs)"))
+                   if world > 1 else "single GPU"},
         "segments_per_step": seg / (args.steps * world),
         "primary_rays_per_s": round(W * H * args.steps * world / dt, 1),
         "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",

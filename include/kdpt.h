@@ -243,6 +243,13 @@ int kdpt_wave_profile(kdpt_ctx *ctx, unsigned long long *out, int n);
 int kdpt_selftest_math(const float *x, int n, float *sin_out, float *cos_out);
 int kdpt_selftest_rng(const int *iter_idx_depth, int n, int k, float *u_out);
 int kdpt_selftest_fresnel(const float *cosines, int n, float ior, float *f_out);
+/* The scatter's glibc calls as restated for gfx950 (src/interactions.h:67-83,214): fn 0 acosf(x),
+ * 1 sin((double)x), 2 cos((double)x); results as doubles. */
+int kdpt_selftest_libm(int fn, const float *x, int n, double *out);
+/* Order-independent digest of fn over the float bit patterns first .. first+count-1 (count <= 2^32):
+ * sum mod 2^64 of splitmix64(result bits ^ splitmix64(input bits)); the oracle's orc_libm_digest
+ * computes the same with the host glibc. */
+int kdpt_selftest_libm_digest(int fn, uint32_t first, unsigned long long count, unsigned long long *digest);
 
 /* ---- Host scene building (C++ restatement of the reference's host code) ---- */
 typedef struct kdpt_scene_data kdpt_scene_data;

@@ -984,12 +984,14 @@ KDPT_HD f3 rotateVector(f3 n1, f3 axis, float angle) {  // :44-65
              (-v * dd) * (1 - ca) + y * ca + (w * x - u * z) * sa,
              (-w * dd) * (1 - ca) + z * ca + (-v * x + u * y) * sa);
 }
-// :67-83 -- double cos/sin/acos: non-default (softness/SSS) branches only; device libm,
-// equal to glibc up to the rare double->float rounding boundary (documented tolerance).
+// :67-83.  theta and phi are float values widened to double; glm::cos/glm::sin on them are glibc's
+// double cos/sin and glm::acos(float) is acosf -- all three restated bit-exactly (kdpt_math.h).
+// Reached with default flags by any material with transmittance > 0 (e.g. the reference's own
+// scenes/stanford_bunny.mtl, Tf 1.0 0.7 0.7) and by the soft lobes when softness > 0.
 KDPT_HD f3 randSphericalVec(float angle, Rng& rng) {
   double theta = 2 * PI_F * u01(rng);
-  double phi = acosf((angle * PI_F * u01(rng) - 1.0f));
-  f3 V = mk3((float)(cos(theta) * sin(phi)), (float)(sin(theta) * sin(phi)), (float)cos(phi));
+  double phi = kdpt_acosf((angle * PI_F * u01(rng) - 1.0f));
+  f3 V = mk3((float)(kdpt_cos(theta) * kdpt_sin(phi)), (float)(kdpt_sin(theta) * kdpt_sin(phi)), (float)kdpt_cos(phi));
   return normalize(V);
 }
 KDPT_HD float getFresnelVal(f3 I, f3 N, float R0) {  // :127-133
@@ -998,7 +1000,7 @@ KDPT_HD float getFresnelVal(f3 I, f3 N, float R0) {  // :127-133
 }
 KDPT_HD f3 soft_lobe(f3 dir, Rng& rng) {
   f3 v = randSphericalVec(0.02f, rng);
-  float angle = acosf(dot(mk3(0.0f, 0.0f, -1.0f), dir));
+  float angle = kdpt_acosf(dot(mk3(0.0f, 0.0f, -1.0f), dir));
   f3 axis = normalize(cross(mk3(0.0f, 0.0f, -1.0f), dir));
   return rotateVector(v, axis, angle);
 }
@@ -1008,7 +1010,7 @@ KDPT_HD void scatterRay(Ray& ray, f3 intersect, f3 normal, const DevMaterial& m,
     float randval = u01(rng);
     if (randval < 0.5f && !ray.isinside) {
       f3 v = randSphericalVec(0.0001f, rng);
-      float angle = acosf(dot(mk3(0.0f, 0.0f, -1.0f), ray.direction));
+      float angle = kdpt_acosf(dot(mk3(0.0f, 0.0f, -1.0f), ray.direction));
       f3 axis = normalize(cross(mk3(0.0f, 0.0f, -1.0f), ray.direction));
       ray.direction = rotateVector(v, axis, angle);
       ray.origin = add(ray.origin, scl(ray.direction, 0.0001f));

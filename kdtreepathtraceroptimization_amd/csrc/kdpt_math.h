@@ -15,7 +15,9 @@
 #if defined(__HIPCC__) || defined(__HIP__)
 #include <hip/hip_runtime.h>
 #define KDPT_HD __host__ __device__ inline
+#define KDPT_HDI __host__ __device__ inline __attribute__((always_inline))
 #else
+#define KDPT_HDI static inline
 #define KDPT_HD static inline
 #include <math.h>
 // host-only builds (tests/native differential harness): HIP's vector types
@@ -230,6 +232,193 @@ KDPT_HD double pow5(double x) {
   double x5 = x4 * x;
   double x5e = dfma(x4, x, -x5) + x4e * x;
   return x5 + x5e;
+}
+
+// ---- glibc 2.35 acosf (sysdeps/ieee754/flt-32/e_acosf.c, the fdlibm float version; the
+//      libm.so.6 code is plain SSE single precision, no FMA variant).  Constants are the
+//      fdlibm words.  Used by randSphericalVec / the soft lobe / fake SSS (src/interactions.h:73,
+//      214, 266-...).  |x| > 1 (possible when a normalised direction's z rounds above 1): glibc's
+//      wrapper returns the quiet NaN 0x7fc00000 (__kernel_standard_f, acosf domain error); a NaN
+//      input comes back quietened.
+KDPT_HDI float kdpt_acosf(float x) {
+  const float one = 1.0f, pi = u2f(0x40490fdau), pio2_hi = u2f(0x3fc90fdau), pio2_lo = u2f(0x33a22168u);
+  const float pS0 = u2f(0x3e2aaaabu), pS1 = u2f(0xbea6b090u), pS2 = u2f(0x3e4e0aa8u), pS3 = u2f(0xbd241146u),
+              pS4 = u2f(0x3a4f7f04u), pS5 = u2f(0x3811ef08u);
+  const float qS1 = u2f(0xc019d139u), qS2 = u2f(0x4001572du), qS3 = u2f(0xbf303361u), qS4 = u2f(0x3d9dc62eu);
+  const int32_t hx = (int32_t)f2u(x);
+  const int32_t ix = hx & 0x7fffffff;
+  if (ix == 0x3f800000) {  // |x| == 1
+    if (hx > 0) return 0.0f;
+    return pi + 2.0f * pio2_lo;
+  } else if (ix > 0x7f800000) {
+    return u2f((uint32_t)hx | 0x00400000u);  // NaN in: (x - x) / (x - x), the input quietened
+  } else if (ix > 0x3f800000) {
+    return u2f(0x7fc00000u);  // |x| > 1: the wrapper's domain-error NaN
+  }
+  if (ix < 0x3f000000) {  // |x| < 0.5
+    if (ix <= 0x32800000) return pio2_hi + pio2_lo;
+    float z = x * x;
+    float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    float r = p / q;
+    return pio2_hi - (x - (pio2_lo - x * r));
+  } else if (hx < 0) {  // x < -0.5
+    float z = (one + x) * 0.5f;
+    float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    float s = sqrtf(z);
+    float r = p / q;
+    float w = r * s - pio2_lo;
+    return pi - 2.0f * (s + w);
+  } else {  // x > 0.5
+    float z = (one - x) * 0.5f;
+    float s = sqrtf(z);
+    float df = u2f(f2u(s) & 0xfffff000u);
+    float c = (z - df * df) / (s + df);
+    float p = z * (pS0 + z * (pS1 + z * (pS2 + z * (pS3 + z * (pS4 + z * pS5)))));
+    float q = one + z * (qS1 + z * (qS2 + z * (qS3 + z * qS4)));
+    float r = p / q;
+    float w = r * s + c;
+    return 2.0f * (df + w);
+  }
+}
+
+// ---- glibc 2.35 double sin / cos (sysdeps/ieee754/dbl-64/s_sin.c: do_sin, do_cos,
+//      reduce_sincos, TAYLOR_SIN; constants usncs.h), as the x86_64 FMA ifunc variant
+//      (__sin_fma / __cos_fma, built with -mfma -mavx2) evaluates it: the products GCC fused
+//      into vfmadd/vfnmadd/vfmsub are the dfma() calls below, everything else is a single
+//      IEEE double op.  Read off the libm.so.6 machine code; checked against glibc on every
+//      float argument below 8 (tests/test_libm_restated.py).  Arguments |x| >= 105414350
+//      (glibc's __branred path) are outside the reference's use (theta < 2 pi, phi <= pi) and
+//      return NaN here.
+}  // namespace kdpt
+#include "glibc_sincostab.h"
+namespace kdpt {
+// The table lives in constant memory on the device (a constexpr array indexed at run time would be
+// copied into every lane's scratch) and as a plain array on the host.
+#if defined(__HIPCC__) || defined(__HIP__)
+static __device__ __constant__ double GLIBC_SINCOSTAB_DEV[KDPT_GLIBC_SINCOSTAB_N] = {KDPT_GLIBC_SINCOSTAB_INIT};
+#endif
+static const double GLIBC_SINCOSTAB_HOST[KDPT_GLIBC_SINCOSTAB_N] = {KDPT_GLIBC_SINCOSTAB_INIT};
+KDPT_HD const double* glibc_sincostab() {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return GLIBC_SINCOSTAB_DEV;
+#else
+  return GLIBC_SINCOSTAB_HOST;
+#endif
+}
+KDPT_HD uint64_t d2u(double d) {
+  uint64_t u;
+  memcpy(&u, &d, 8);
+  return u;
+}
+KDPT_HD double u2d(uint64_t u) {
+  double d;
+  memcpy(&d, &u, 8);
+  return d;
+}
+KDPT_HD double dabs(double x) { return u2d(d2u(x) & 0x7fffffffffffffffull); }
+KDPT_HD double dcopysign(double m, double s) {
+  return u2d((d2u(m) & 0x7fffffffffffffffull) | (d2u(s) & 0x8000000000000000ull));
+}
+namespace glibc_sin {
+constexpr double sn3 = -0x1.5555555555515p-3, sn5 = 0x1.11110e829872fp-7;
+constexpr double cs2 = 0x1.0p-1, cs4 = -0x1.5555555555535p-5, cs6 = 0x1.6c16bedd9e239p-10;
+constexpr double s1 = -0x1.5555555555555p-3, s2 = 0x1.1111111110ecep-7, s3 = -0x1.a01a019db08b8p-13,
+                 s4 = 0x1.71de27b9a7ed9p-19, s5 = -0x1.addffc2fcdf59p-26;
+constexpr double big = 0x1.8p45, hp0 = 0x1.921fb54442d18p0, hp1 = 0x1.1a62633145c07p-54;
+constexpr double mp1 = 0x1.921fb58p0, mp2 = -0x1.dde973cp-27, pp3 = -0x1.cb3b398p-55,
+                 pp4 = -0x1.d747f23e32ed7p-83, hpinv = 0x1.45f306dc9c883p-1, toint = 0x1.8p52;
+}  // namespace glibc_sin
+// TAYLOR_SIN(xx, a, da): a + (xx * (P(xx) * a - 0.5 * da) + da), P = s1 + xx*(s2 + ...)
+KDPT_HDI double glibc_taylor_sin(double xx, double a, double da) {
+  using namespace glibc_sin;
+  double p = dfma(xx, dfma(xx, dfma(xx, dfma(xx, s5, s4), s3), s2), s1);
+  double t = dfma(xx, dfma(p, a, -(0.5 * da)), da);
+  return a + t;
+}
+KDPT_HDI double glibc_do_sin(double x, double dx) {
+  using namespace glibc_sin;
+  const double xold = x;
+  if (dabs(x) < 0.126) return glibc_taylor_sin(x * x, x, dx);
+  if (x <= 0) dx = -dx;
+  const double ax = dabs(x);
+  const double u = big + ax;
+  const int k = (int)(uint32_t)d2u(u) << 2;
+  x = ax - (u - big);
+  const double xx = x * x;
+  const double s = x + dfma(x * xx, dfma(xx, sn5, sn3), dx);
+  const double c = dfma(x, dx, xx * dfma(xx, dfma(xx, cs6, cs4), cs2));
+  const double* tab = glibc_sincostab();
+  const double sn = tab[k], ssn = tab[k + 1], cs = tab[k + 2], ccs = tab[k + 3];
+  const double cor = dfma(s, cs, dfma(-c, sn, dfma(s, ccs, ssn)));
+  return dcopysign(sn + cor, xold);
+}
+KDPT_HDI double glibc_do_cos(double x, double dx) {
+  using namespace glibc_sin;
+  if (x < 0) dx = -dx;
+  const double ax = dabs(x);
+  const double u = big + ax;
+  const int k = (int)(uint32_t)d2u(u) << 2;
+  x = (ax - (u - big)) + dx;
+  const double xx = x * x;
+  const double s = dfma(x * xx, dfma(xx, sn5, sn3), x);
+  const double c = xx * dfma(xx, dfma(xx, cs6, cs4), cs2);
+  const double* tab = glibc_sincostab();
+  const double sn = tab[k], ssn = tab[k + 1], cs = tab[k + 2], ccs = tab[k + 3];
+  const double cor = dfma(-s, sn, dfma(-c, cs, dfma(-s, ssn, ccs)));
+  return cs + cor;
+}
+// reduce_sincos: x = n * pi/2 + (a + da), |x| < 105414350; returns n & 3
+KDPT_HDI int glibc_reduce_sincos(double x, double* a, double* da) {
+  using namespace glibc_sin;
+  const double t = dfma(x, hpinv, toint);
+  const double xn = t - toint;
+  const int n = (int)(d2u(t) & 3u);
+  double y = dfma(-xn, mp1, x);
+  y = dfma(-xn, mp2, y);
+  const double t2 = dfma(-xn, pp3, y);
+  double db = dfma(-pp3, xn, y - t2);
+  const double b = dfma(-xn, pp4, t2);
+  db = db + dfma(-xn, pp4, t2 - b);
+  *a = b;
+  *da = db;
+  return n;
+}
+KDPT_HDI double glibc_do_sincos(double a, double da, int n) {
+  double r = (n & 1) ? glibc_do_cos(a, da) : glibc_do_sin(a, da);
+  return (n & 2) ? -r : r;
+}
+KDPT_HDI double kdpt_sin(double x) {
+  using namespace glibc_sin;
+  const uint32_t k = (uint32_t)(d2u(x) >> 32) & 0x7fffffffu;
+  if (k < 0x3e500000u) return x;
+  if (k < 0x3feb6000u) return glibc_do_sin(x, 0.0);
+  if (k < 0x400368fdu) return dcopysign(glibc_do_cos(hp0 - dabs(x), hp1), x);
+  if (k < 0x419921fbu) {
+    double a, da;
+    int n = glibc_reduce_sincos(x, &a, &da);
+    return glibc_do_sincos(a, da, n);
+  }
+  return u2d(0x7ff8000000000000ull);
+}
+KDPT_HDI double kdpt_cos(double x) {
+  using namespace glibc_sin;
+  const uint32_t k = (uint32_t)(d2u(x) >> 32) & 0x7fffffffu;
+  if (k < 0x3e400000u) return 1.0;
+  if (k < 0x3feb6000u) return glibc_do_cos(x, 0.0);
+  if (k < 0x400368fdu) {
+    const double y = hp0 - dabs(x);
+    const double a = y + hp1;
+    const double da = (y - a) + hp1;
+    return glibc_do_sin(a, da);
+  }
+  if (k < 0x419921fbu) {
+    double a, da;
+    int n = glibc_reduce_sincos(x, &a, &da);
+    return glibc_do_sincos(a, da, n + 1);
+  }
+  return u2d(0x7ff8000000000000ull);
 }
 
 // ---- RNG: utilhash (src/intersections.h:15-23), thrust minstd_rand (a=48271,

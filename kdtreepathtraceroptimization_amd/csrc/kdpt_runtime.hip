@@ -215,7 +215,7 @@ __device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, 
 // before the KD tree; src/pathtrace.cu:1600-1640) -> t_min / hit, and the traversal's first step, the
 // KD root's box (same intersectAABB, same invdir): false = the traversal ends there.
 constexpr int ORDERED_GEOMS = 8;  // scenes with at most this many analytic geoms test them nearest-first
-__device__ inline bool prep_ray(const DevScene& S, bool kd, f3 o, f3 d, float& t_min, int& hit) {
+__device__ __attribute__((always_inline)) inline bool prep_ray(const DevScene& S, bool kd, f3 o, f3 d, float& t_min, int& hit) {
   Ray ray;
   ray.origin = o;
   ray.direction = d;
@@ -743,7 +743,7 @@ struct ShadeOut {
 };
 
 template <bool HYBRID, bool COMPACT>
-__device__ inline void shade_one(const ShadeArgs& A, const DevScene& S, int i, ShadeOut& o) {
+__device__ __attribute__((always_inline)) inline void shade_one(const ShadeArgs& A, const DevScene& S, int i, ShadeOut& o) {
   const float4 q0 = A.paths.p0[i], q1 = A.paths.p1[i], q2 = A.paths.p2[i];
   int matHit = A.paths.pm[i];
   // issued with the path loads (every listed slot has a record; unused when the path has no bounces
@@ -1220,6 +1220,32 @@ __global__ void k_unpack(PathBuf src, const int* counts, int depth, kdpt_path_se
 __global__ void k_selftest_math(const float* x, int n, float* so, float* co) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i < n) { so[i] = kdpt_sinf(x[i]); co[i] = kdpt_cosf(x[i]); }
+}
+// glibc acosf / sin / cos restatements (kdpt_math.h): fn 0 acosf(x), 1 sin((double)x), 2 cos((double)x)
+__device__ inline uint64_t libm_bits(int fn, float x) {
+  if (fn == 0) return f2u(kdpt_acosf(x));
+  return d2u(fn == 1 ? kdpt_sin((double)x) : kdpt_cos((double)x));
+}
+__device__ inline uint64_t splitmix64(uint64_t z) {
+  z += 0x9e3779b97f4a7c15ull;
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+__global__ void k_selftest_libm(int fn, const float* x, int n, double* out) {
+  int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  uint64_t b = libm_bits(fn, x[i]);
+  out[i] = fn == 0 ? (double)u2f((uint32_t)b) : u2d(b);
+}
+__global__ void k_selftest_libm_digest(int fn, uint32_t first, uint64_t count, unsigned long long* acc) {
+  uint64_t sum = 0;
+  const uint64_t stride = (uint64_t)gridDim.x * blockDim.x;
+  for (uint64_t k = (uint64_t)blockIdx.x * blockDim.x + threadIdx.x; k < count; k += stride) {
+    const uint32_t xb = (uint32_t)(first + k);
+    sum += splitmix64(libm_bits(fn, u2f(xb)) ^ splitmix64(xb));
+  }
+  atomicAdd(acc, (unsigned long long)sum);
 }
 __global__ void k_selftest_rng(const int* iid, int n, int k, float* u) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
@@ -2385,6 +2411,34 @@ int kdpt_selftest_math(const float* x, int n, float* so, float* co) {
   HIP_TRY(hipMemcpy(so, ds, sizeof(float) * n, hipMemcpyDeviceToHost));
   HIP_TRY(hipMemcpy(co, dc, sizeof(float) * n, hipMemcpyDeviceToHost));
   (void)hipFree(dx); (void)hipFree(ds); (void)hipFree(dc);
+  return KDPT_OK;
+}
+
+int kdpt_selftest_libm(int fn, const float* x, int n, double* out) {
+  if (fn < 0 || fn > 2 || n < 0 || (n && (!x || !out))) return fail(KDPT_ERR_ARG, "kdpt_selftest_libm: bad arguments");
+  if (n == 0) return KDPT_OK;
+  float* dx;
+  double* dout;
+  HIP_TRY(hipMalloc((void**)&dx, sizeof(float) * n));
+  HIP_TRY(hipMalloc((void**)&dout, sizeof(double) * n));
+  HIP_TRY(hipMemcpy(dx, x, sizeof(float) * n, hipMemcpyHostToDevice));
+  hipLaunchKernelGGL(k_selftest_libm, dim3((n + 255) / 256), dim3(256), 0, 0, fn, dx, n, dout);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(out, dout, sizeof(double) * n, hipMemcpyDeviceToHost));
+  (void)hipFree(dx); (void)hipFree(dout);
+  return KDPT_OK;
+}
+
+int kdpt_selftest_libm_digest(int fn, uint32_t first, unsigned long long count, unsigned long long* digest) {
+  if (fn < 0 || fn > 2 || !digest || count > (1ull << 32) || first + count > (1ull << 32))
+    return fail(KDPT_ERR_ARG, "kdpt_selftest_libm_digest: bad arguments");
+  unsigned long long* dacc;
+  HIP_TRY(hipMalloc((void**)&dacc, sizeof(unsigned long long)));
+  HIP_TRY(hipMemset(dacc, 0, sizeof(unsigned long long)));
+  hipLaunchKernelGGL(k_selftest_libm_digest, dim3(4096), dim3(256), 0, 0, fn, first, (uint64_t)count, dacc);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(digest, dacc, sizeof(unsigned long long), hipMemcpyDeviceToHost));
+  (void)hipFree(dacc);
   return KDPT_OK;
 }
 

@@ -20,9 +20,20 @@ def shard_iterations(first_step: int, steps: int, world: int, rank: int) -> list
 
 
 def reduce_image(image, dist, dst: int = 0):
-    """Sum the ranks' accumulation buffers into `dst` (in place on `image`, a torch tensor)."""
-    if dist is not None and dist.is_initialized() and dist.get_world_size() > 1:
-        dist.reduce(image, dst=dst, op=dist.ReduceOp.SUM)
+    """Sum the ranks' accumulation buffers into `dst` (in place on `image`, a torch tensor).
+
+    With the "nccl" backend (RCCL) the device buffer is reduced in place over xGMI.  The "gloo" backend
+    (CPU rehearsals, and several ranks sharing one GPU, which RCCL refuses) reduces a host copy, which
+    is written back into the device buffer on `dst`."""
+    if dist is None or not dist.is_initialized() or dist.get_world_size() < 2:
+        return image
+    if image.is_cuda and dist.get_backend() == "gloo":
+        host = image.cpu()
+        dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM)
+        if dist.get_rank() == dst:
+            image.copy_(host)
+        return image
+    dist.reduce(image, dst=dst, op=dist.ReduceOp.SUM)
     return image
 
 

@@ -291,6 +291,40 @@ void orc_sincos_array(const float *x, int n, float *s, float *c) {
 #pragma omp parallel for schedule(static)
     for (int i = 0; i < n; i++) { s[i] = sinf(x[i]); c[i] = cosf(x[i]); }
 }
+/* glibc acosf / sin / cos as the reference's soft-lobe and fake-SSS scatter calls them
+   (src/interactions.h:67-83,214): fn 0 acosf(x), 1 sin((double)x), 2 cos((double)x). */
+static uint64_t libm_bits(int fn, float x) {
+    if (fn == 0) { float r = acosf(x); uint32_t u; memcpy(&u, &r, 4); return u; }
+    double r = fn == 1 ? sin((double)x) : cos((double)x);
+    uint64_t u;
+    memcpy(&u, &r, 8);
+    return u;
+}
+static uint64_t splitmix64(uint64_t z) {
+    z += 0x9e3779b97f4a7c15ull;
+    z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+    z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+    return z ^ (z >> 31);
+}
+void orc_libm_array(int fn, const float *x, int n, double *out) {
+#pragma omp parallel for schedule(static)
+    for (int i = 0; i < n; i++) {
+        uint64_t b = libm_bits(fn, x[i]);
+        if (fn == 0) { float r; uint32_t u = (uint32_t)b; memcpy(&r, &u, 4); out[i] = r; }
+        else memcpy(&out[i], &b, 8);
+    }
+}
+uint64_t orc_libm_digest(int fn, uint32_t first, uint64_t count) {
+    uint64_t acc = 0;
+#pragma omp parallel for reduction(+ : acc) schedule(static, 1 << 16)
+    for (int64_t k = 0; k < (int64_t)count; k++) {
+        uint32_t xb = (uint32_t)(first + (uint64_t)k);
+        float x;
+        memcpy(&x, &xb, 4);
+        acc += splitmix64(libm_bits(fn, x) ^ splitmix64(xb));
+    }
+    return acc;
+}
 void orc_u01_array(const int *iid, int n, int k, float *u) {
     for (int i = 0; i < n; i++) u[i] = orc_u01_sequence(iid[3 * i], iid[3 * i + 1], iid[3 * i + 2], k);
 }

@@ -230,6 +230,11 @@ float orc_cosf(float x);
 void orc_sincos_array(const float *x, int n, float *s, float *c);
 /* u01 draws: for each (iter, index, depth) triple, the k-th uniform of makeSeededRandomEngine */
 void orc_u01_array(const int *iid, int n, int k, float *u);
+/* glibc acosf(x) (fn 0), sin((double)x) (1), cos((double)x) (2), as doubles */
+void orc_libm_array(int fn, const float *x, int n, double *out);
+/* order-independent digest of fn over the float bit patterns first .. first+count-1:
+   sum of splitmix64(result bits ^ splitmix64(input bits)) (kdpt_selftest_libm_digest computes the same) */
+uint64_t orc_libm_digest(int fn, uint32_t first, uint64_t count);
 /* getFresnelVal with dot(N,-I) == cosines[i] */
 void orc_fresnel_array(const float *cosines, int n, float ior, float *f);
 

@@ -100,6 +100,9 @@ def lib():
         L.orc_cosf.argtypes = [C.c_float]
         L.orc_cosf.restype = C.c_float
         L.orc_sincos_array.argtypes = [P(C.c_float), C.c_int, P(C.c_float), P(C.c_float)]
+        L.orc_libm_array.argtypes = [C.c_int, P(C.c_float), C.c_int, P(C.c_double)]
+        L.orc_libm_digest.argtypes = [C.c_int, C.c_uint32, C.c_uint64]
+        L.orc_libm_digest.restype = C.c_uint64
         L.orc_u01_array.argtypes = [P(C.c_int), C.c_int, C.c_int, P(C.c_float)]
         L.orc_fresnel_array.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
         L.orc_trace_ray.argtypes = [P(OScene), P(C.c_float), P(C.c_float), C.c_int, P(C.c_double)]
@@ -256,6 +259,18 @@ def sincos(x: np.ndarray):
     s, c = np.empty_like(x), np.empty_like(x)
     lib().orc_sincos_array(_fp(x), len(x), _fp(s), _fp(c))
     return s, c
+
+
+def libm(fn: int, x: np.ndarray):
+    """glibc acosf(x) (fn 0), sin((double)x) (1), cos((double)x) (2) as float64."""
+    x = np.ascontiguousarray(x, np.float32)
+    out = np.empty(len(x), np.float64)
+    lib().orc_libm_array(fn, _fp(x), len(x), out.ctypes.data_as(C.POINTER(C.c_double)))
+    return out
+
+
+def libm_digest(fn: int, first: int, count: int) -> int:
+    return int(lib().orc_libm_digest(fn, first, count))
 
 
 def u01(iid: np.ndarray, k: int):

@@ -1,0 +1,39 @@
+"""The gfx950 build's per-kernel resource report (hipcc -Rpass-analysis=kernel-resource-usage, written to
+build/kdpt_runtime.build.log by kdtreepathtraceroptimization_amd/_build.py): the hot kernels must not use
+scratch (register spills or out-of-line calls, which also cap occupancy) and must keep their occupancy."""
+import os
+import re
+
+import pytest
+
+from kdtreepathtraceroptimization_amd import _build
+
+
+def _report():
+    if not os.path.exists(_build.RESOURCE_LOG):
+        _build.build(force=True)
+    out, cur = {}, None
+    for line in open(_build.RESOURCE_LOG):
+        m = re.search(r"Function Name: (\S+)", line)
+        if m:
+            cur = m.group(1)
+            out[cur] = {}
+            continue
+        m = re.search(r"remark:\s+(VGPRs|ScratchSize \[bytes/lane\]|Occupancy \[waves/SIMD\]): (\d+)", line)
+        if m and cur:
+            out[cur][m.group(1).split()[0]] = int(m.group(2))
+    return out
+
+
+# kernel name fragment -> minimum waves per SIMD
+HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_shade_fused": 6, "k_geoms": 4, "k_gen_rays": 4}
+
+
+@pytest.mark.parametrize("frag", sorted(HOT))
+def test_hot_kernels_no_scratch(kdpt, frag):
+    rep = _report()
+    ks = [k for k in rep if frag in k]
+    assert ks, frag
+    for k in ks:
+        assert rep[k].get("ScratchSize", 0) == 0, (k, rep[k])
+        assert rep[k].get("Occupancy", 0) >= HOT[frag], (k, rep[k])

@@ -115,3 +115,18 @@ def test_oracle_files_equal_fixture(oracle, mesh):
     b = oracle.OracleScene.from_description(load_fixture_scene("cornell", mesh))
     for m in ("nodes_bytes", "tris_bytes", "geoms_bytes", "materials_bytes", "camera_bytes"):
         assert getattr(a, m)() == getattr(b, m)(), m
+
+
+def test_oracle_reproduces_committed_fullsize_pins(oracle):
+    """The oracle here reproduces tests/golden/oracle_anchors.json (first iteration of every config), the
+    pins the GPU full-size tests compare against (tests/test_gpu_fullsize.py)."""
+    import json
+    with open(os.path.join(FIXTURE_DIR, "oracle_anchors.json")) as f:
+        cfgs = json.load(f)["configs"]
+    for c in cfgs:
+        s = oracle.OracleScene.from_description(load_fixture_scene(c["scene"], c["mesh"], res=c["res"],
+                                                                   depth=c["depth"]))
+        rec = c["iterations"][0]
+        im, st = s.render(rec["iter"], 1, **c["options"])
+        assert st.segments == rec["segments"], c["id"]
+        assert hashlib.sha256(im.tobytes()).hexdigest() == rec["sha256"], c["id"]
