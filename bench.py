@@ -1,31 +1,33 @@
 """bench.py -- the reference's headline metric on MI355X.
 
-Metric (BASELINE.json): Mrays/s at 800x800, depth 8, cornell + dragon (dragon_5.obj: the
-only dragon mesh present -- cornell9.txt does not exist).
-A step = one iteration = one sample per pixel through the whole hot path
-(camera rays -> up to 8 x [intersect + KD traversal + scatter + shade + gather +
-stable compaction]).  Mrays/s = path segments launched into the intersect kernel,
-summed over all ranks, / the max-over-ranks wall time of the K timed steps.
+Metric (BASELINE.json): Mrays/s at 800x800, depth 8, cornell + dragon (dragon_5.obj: the only dragon mesh
+present -- cornell9.txt does not exist), plus ms per iteration.
 
-Multi-GPU (one process per GPU, `torch.distributed.run`): samples per pixel shard
-across ranks (rank r renders global iterations r+1, r+1+N, ...: weak scaling) and the
-float3 accumulation images are summed on rank 0 with one RCCL reduce over xGMI inside
-the timed region.
+A step is one frame of `--spp-per-step` samples per pixel (default 16): that many iterations of the whole
+hot path (camera rays -> up to 8 x [intersect + KD traversal + scatter + shade + gather + stable
+compaction]), each a distinct global iteration number (its own RNG seed).  Mrays/s = path segments
+launched into the intersect stage, summed over all ranks, / the max-over-ranks wall time of the K timed
+steps.  Iterations stay in flight across the frame (kdpt_trace_iterations), so a frame of 16 samples
+keeps the GPU at steady state; `ms_per_iteration` is reported beside `ms_per_step`.
 
-Roofline: the dominant kernel is k_trace, the KD traversal of the rays that meet the KD root box (the
-analytic geoms and the root-box test of every ray run before it: in k_geoms for camera rays, fused into the
-previous bounce's shading/compaction otherwise; a ray that misses the root box ends there).  HBM-bound
-framing with SURVEY.md 8(d)'s per-segment bytes B = 352 + 52*N_aabb + 36*N_tri + 40*N_hit restricted to the
-traversal k_trace performs: per counting iteration 76*n_k + 52*(N_aabb - N_root_miss) + 36*N_tri + 40*N_hit
-(n_k = segments handed to k_trace, 76 = PathSegment read 56 + ShadeableIntersection write 20), scaled to the
-timed segments; achieved = bytes per launch / the average k_trace launch time on the device clock inside the
-kernel (first workgroup start to last workgroup end; agrees with rocprofv3's kernel-trace durations).  HIP
-events around the intersect stage are reported beside it: with several iterations in flight they also
-count the time a launch waits behind the other iterations' kernels.
+Multi-GPU (one process per GPU, `torch.distributed.run`): samples per pixel shard across ranks (rank r
+renders global iterations r+1, r+1+N, ...: weak scaling) and the float3 accumulation images are summed on
+rank 0 with one RCCL reduce over xGMI inside the timed region.
+
+Roofline: the dominant kernel is k_trace (the KD traversal of the rays that meet the KD root box).  It is
+bound by VALU issue and latency, not HBM (its tree lives in LDS, its triangles in L2), so the
+roofline is VALU issue: peak = 256 CUs x 4 SIMDs x 1/2 wave64 VALU instruction per clock x 2.4 GHz.
+achieved = k_trace's VALU wave-instructions per launch / (launch duration x the grid share the launch ran
+on): the instructions per k_trace ray come from rocprofv3 SQ_INSTS_VALU of the same kernel sources
+(profiles/pmc_<workload>.json, matched by a hash of the kernel sources -- null when stale), the rays per
+launch and the launch duration are measured live (device counters, s_memrealtime).  traffic = HBM bytes
+per launch from the same profile (FETCH_SIZE x 2, the gfx950 correction of MI355X_MICROARCH.md, +
+WRITE_SIZE), scaled to the live rays per launch.
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
 import os
 import sys
@@ -33,21 +35,25 @@ import time
 
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
-# kdpt_trace_iterations keeps `--pipeline` iterations in flight on their own HIP streams plus one
-# accumulation stream; HIP's default of 4 hardware queues per process would make some of them share
-# a queue (and serialise), so ask for 16 before the runtime initialises.
+# kdpt_trace_iterations keeps `--pipeline` batches in flight on their own HIP streams plus one accumulation
+# stream; HIP's default of 4 hardware queues per process would make some of them share a queue (and
+# serialise), so ask for 16 (<= 32) before the runtime initialises.
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
     os.environ["GPU_MAX_HW_QUEUES"] = "16"
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
+# VALU issue: 256 CUs x 4 SIMD-32 x one wave64 instruction per 2 clocks x 2.4 GHz (MI355X_MICROARCH.md)
+VALU_PEAK_GINST = 256 * 4 * 0.5 * 2.4
+KERNEL_SOURCES = ["kdpt_device.h", "kdpt_math.h", "kdpt_runtime.hip", "glibc_sincostab.h"]
 
 
 def parse():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=192)
-    ap.add_argument("--warmup", type=int, default=8)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--spp-per-step", type=int, default=16, help="iterations (samples per pixel) per step")
     ap.add_argument("--mesh", default="dragon_5")
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--res", type=int, nargs=2, default=(800, 800))
@@ -63,16 +69,44 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = host-side reduce, for rehearsing the "
                          "N > 1 path with several ranks sharing one GPU")
+    ap.add_argument("--pmc-profile", default=None, help="profile JSON for the VALU roofline (default: "
+                    "profiles/pmc_<scene>_<mesh>_<W>x<H>.json)")
     return ap.parse_args()
 
 
+def kernel_source_hash() -> str:
+    h = hashlib.sha256()
+    for f in KERNEL_SOURCES:
+        h.update(open(os.path.join(ROOT, "kdtreepathtraceroptimization_amd", "csrc", f), "rb").read())
+    return h.hexdigest()[:16]
+
+
+def host_info():
+    model = ""
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                model = line.split(":", 1)[1].strip()
+                break
+    except OSError:
+        pass
+    aff = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else (os.cpu_count() or 1)
+    omp = os.environ.get("OMP_NUM_THREADS")
+    return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": omp}
+
+
 def cpu_baseline(args, threads=None, seconds=None):
-    """The oracle (plain-C port of the reference path) on this host's cores, bounded sample."""
+    """The oracle (plain-C port of the reference path, OpenMP over paths) on this host's cores, on a
+    bounded sample of the same workload.  Threads: every CPU this process may run on, capped by
+    OMP_NUM_THREADS when the environment sets it (the GPU box allots 16 host CPUs per GPU and sets it)."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     from kdtreepathtraceroptimization_amd.fixtures import load_fixture_scene
+    info = host_info()
     if threads is None:
-        threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(16, os.cpu_count() or 1)
+        threads = info["affinity_cpus"]
+        if info["omp_num_threads"]:
+            threads = max(1, min(threads, int(info["omp_num_threads"])))
     seconds = args.cpu_seconds if seconds is None else seconds
     s = oracle_lib.OracleScene.from_description(
         load_fixture_scene(args.scene, args.mesh, res=tuple(args.res), depth=args.depth))
@@ -85,7 +119,38 @@ def cpu_baseline(args, threads=None, seconds=None):
         it += 1
     return {"value": round(seg / t / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
             "sample": f"oracle (plain-C restatement of the reference's host-side kernels), {it - 3} iteration(s) "
-                      f"3..{it - 1} of the same workload, {t:.1f} s, OpenMP over paths"}
+                      f"3..{it - 1} of the same workload, {t:.1f} s, OpenMP over paths, {threads} thread(s)",
+            "host": info}
+
+
+def valu_roofline(args, W, H, rays_per_launch, launch_ms, share):
+    """VALU-issue roofline of one k_trace launch from the committed PMC profile (see module docstring)."""
+    path = args.pmc_profile or os.path.join(ROOT, "profiles", f"pmc_{args.scene}_{args.mesh}_{W}x{H}.json")
+    out = {"bound": "valu-issue", "unit": "G VALU wave-instructions/s", "peak": VALU_PEAK_GINST,
+           "achieved": None, "frac": None, "traffic": None, "kernel": "k_trace",
+           "pmc_source": os.path.relpath(path, ROOT)}
+    src = kernel_source_hash()
+    if not os.path.exists(path):
+        out["note"] = "no PMC profile for this workload"
+        return out
+    prof = json.load(open(path))
+    k = prof.get("kernels", {}).get("k_trace")
+    if prof.get("kernel_source_sha") != src or not k:
+        out["note"] = f"PMC profile is for kernel sources {prof.get('kernel_source_sha')}, not {src}: stale"
+        return out
+    inst = k["valu_per_ray"] * rays_per_launch
+    eff_s = launch_ms * 1e-3 * share  # the launch ran on `share` of the chip's CUs
+    out["achieved"] = round(inst / eff_s / 1e9, 2) if eff_s > 0 else None
+    out["frac"] = round(out["achieved"] / VALU_PEAK_GINST, 4) if out["achieved"] else None
+    if k.get("hbm_bytes_per_ray") is not None:
+        out["traffic"] = round(k["hbm_bytes_per_ray"] * rays_per_launch)
+        out["traffic_GBps"] = round(out["traffic"] / (launch_ms * 1e-3) / 1e9, 2) if launch_ms > 0 else None
+        out["traffic_hbm_frac"] = round(out["traffic_GBps"] / HBM_PEAK_GBS, 4) if out["traffic_GBps"] else None
+    out["valu_inst_per_launch"] = round(inst)
+    out["valu_per_ray"] = k["valu_per_ray"]
+    out["pmc_exclusive_valu_frac"] = k.get("valu_busy_frac")
+    out["kernel_source_sha"] = src
+    return out
 
 
 def main():
@@ -105,7 +170,9 @@ def main():
         else:
             dist.init_process_group("gloo")
     from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options, load_fixture_scene
+    from kdtreepathtraceroptimization_amd.distributed import global_iteration, reduce_image
 
+    S = max(1, args.spp_per_step)
     desc = load_fixture_scene(args.scene, args.mesh, res=tuple(args.res), depth=args.depth)
     sd = SceneData.from_description(desc)
     W, H = sd.resolution
@@ -114,21 +181,16 @@ def main():
                           bounce_cap=args.bounce_cap)
     pt = PathTracer(sd, opt, device=local)
 
-    from kdtreepathtraceroptimization_amd.distributed import global_iteration, reduce_image
+    def first_iter(local_iteration):  # 1-based global iteration of this rank's local iteration j (spp sharding)
+        return global_iteration(local_iteration, world, rank)
 
-    def global_iter(step):  # 1-based, distinct across ranks and steps (spp sharding)
-        return global_iteration(step, world, rank)
-
-    # warmup (iterations disjoint from the timed ones); iteration 2's extra sort lands here
+    # warmup: iterations disjoint from the timed ones (iteration 2's extra sort lands here)
     if args.warmup:
-        pt.trace_iterations(global_iter(0), args.warmup, stride=world, pipeline=args.pipeline, batch=args.batch)
+        pt.trace_iterations(first_iter(0), args.warmup * S, stride=world, pipeline=args.pipeline, batch=args.batch)
         pt.synchronize()
-    # roofline counters from one untimed counting iteration of the timed range
-    aabb, tri, hit = pt.count_iteration(global_iter(args.warmup))
-    try:
-        aabb_prep, cand = pt.count_split()
-    except AttributeError:  # an older libkdpt (A/B runs): no split, the whole stage
-        aabb_prep, cand = 0, None
+    # per-segment work counters from one untimed counting iteration of the timed range (informational)
+    aabb, tri, hit = pt.count_iteration(first_iter(args.warmup * S))
+    aabb_prep, cand = pt.count_split()
     cnt_stats = pt.stats()
     accum.zero_()
     torch.cuda.synchronize()
@@ -137,7 +199,7 @@ def main():
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    pt.trace_iterations(global_iter(args.warmup), args.steps, stride=world, pipeline=args.pipeline,
+    pt.trace_iterations(first_iter(args.warmup * S), args.steps * S, stride=world, pipeline=args.pipeline,
                         batch=args.batch)
     pt.synchronize()
     reduce_image(accum, dist)  # spp shards -> one framebuffer (the only exchange step)
@@ -148,38 +210,44 @@ def main():
     dt = time.perf_counter() - t0
     st1 = pt.stats()
     seg = st1.total_segments - st0.total_segments
-    ev_ms = st1.intersect_ms_total - st0.intersect_ms_total  # HIP events around each intersect launch
-    ev_launches = st1.intersect_launches_total - st0.intersect_launches_total
+    rays = st1.total_trace_rays - st0.total_trace_rays  # handed to k_trace
     kernel_ms = st1.intersect_device_ms_total - st0.intersect_device_ms_total  # device clock, per launch
     launches = st1.intersect_device_launches_total - st0.intersect_device_launches_total
     if dist:
-        t = torch.tensor([dt, float(seg), kernel_ms, float(launches), ev_ms, float(ev_launches)], dtype=torch.float64,
-                         device=f"cuda:{local}" if args.dist_backend == "nccl" else "cpu")
+        dev = f"cuda:{local}" if args.dist_backend == "nccl" else "cpu"
+        t = torch.tensor([dt, float(seg), float(rays), kernel_ms, float(launches)], dtype=torch.float64, device=dev)
         tmax = t[0:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t[1:].clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
-        dt, seg, kernel_ms, launches = float(tmax[0]), int(tsum[0]), float(tsum[1]), int(tsum[2])
-        ev_ms, ev_launches = float(tsum[3]), int(tsum[4])
+        dt = float(tmax[0])
+        seg, rays, kernel_ms, launches = int(tsum[0]), int(tsum[1]), float(tsum[2]), int(tsum[3])
     if rank != 0:
         pt.close()
         if dist:
             dist.destroy_process_group()
         return
-    # roofline of the dominant kernel, k_trace (the KD traversal of the rays that meet the root box), per
-    # launch: algorithmic bytes of the counting iteration's k_trace work, scaled to the timed segments
-    count_seg = max(1, sum(cnt_stats.seg_per_bounce[d] for d in range(32)) or seg // max(1, args.steps * world))
-    cand = count_seg if cand is None else cand
-    aabb_k = aabb - aabb_prep  # the root-box tests of rays that end before k_trace are not its work
-    iter_bytes = 76 * cand + 52 * aabb_k + 36 * tri + 40 * hit
-    per_seg_bytes = iter_bytes / count_seg
+    iters = args.steps * S * world
     avg_launch_ms = kernel_ms / max(1, launches)
-    bytes_per_launch = per_seg_bytes * seg / max(1, launches)
-    achieved = bytes_per_launch / (avg_launch_ms * 1e-3) / 1e9 if avg_launch_ms > 0 else 0.0
-    traffic = None
-    tfile = os.path.join(ROOT, "profiles", f"traffic_{args.scene}_{args.mesh}_{W}x{H}.json")
-    if os.path.exists(tfile):
-        traffic = json.load(open(tfile)).get("hbm_bytes_per_launch")
+    rays_per_launch = rays / max(1, launches)
+    share = pt.trace_grid_share()
+    roof = valu_roofline(args, W, H, rays_per_launch, avg_launch_ms, share)
+    count_seg = max(1, sum(cnt_stats.seg_per_bounce[d] for d in range(32)))
+    alg_bytes = 76 * cand + 52 * (aabb - aabb_prep) + 36 * tri + 40 * hit  # SURVEY 8(d) model, k_trace's part
+    roof.update({
+        "launch_grid_share": round(share, 4), "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
+        "rays_per_launch": round(rays_per_launch, 1),
+        "k_trace_ms_per_step": round(kernel_ms / max(1, args.steps * world), 4),
+        "k_trace_busy_share": round(kernel_ms * share / (dt * 1e3 * world), 4),
+        "algorithmic": {"bytes_per_ray": round(alg_bytes / max(1, cand), 1),
+                        "GBps_per_launch": round(alg_bytes / max(1, cand) * rays_per_launch / (avg_launch_ms * 1e-3)
+                                                 / 1e9, 1) if avg_launch_ms > 0 else None,
+                        "note": "SURVEY 8(d) byte model of k_trace's work; most of these bytes are LDS/L2 hits, "
+                                "so it is not an HBM rate"},
+        "per_segment_counts": {"aabb": round(aabb / count_seg, 4), "tri": round(tri / count_seg, 4),
+                               "hit": round(hit / count_seg, 5), "aabb_before_k_trace": round(aabb_prep / count_seg, 4),
+                               "k_trace_share": round(cand / count_seg, 4)},
+    })
     out = {
         "metric": METRIC,
         "value": round(seg / dt / 1e6, 3),
@@ -192,47 +260,27 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
-        "data": "synthetic camera rays over the reference's own scene assets (cornell.txt + dragon_5.obj, "
-                "parsed fixtures under tests/golden); deterministic RNG seeded by iteration",
+        "data": f"synthetic camera rays over the reference's own scene assets ({args.scene}.txt + {args.mesh}.obj, "
+                "parsed fixtures under tests/golden); deterministic RNG seeded by global iteration",
         "config": {"workload": f"{args.scene}.txt + {args.mesh}.obj, {W}x{H}, depth {args.depth}, "
-                               f"bounce cap {args.bounce_cap}, 1 spp per step "
-                               f"per GPU ({args.pipeline} x {args.batch} iterations in flight), "
+                               f"bounce cap {args.bounce_cap}, {S} spp per step per GPU "
+                               f"({args.pipeline} x {args.batch} iterations in flight), "
                                + ("short-stack hybrid KD traversal" if not args.bare else "bare traversal"),
                    "scene": args.scene, "mesh": args.mesh, "resolution": [W, H], "depth": args.depth,
-                   "bounce_cap": args.bounce_cap,
+                   "bounce_cap": args.bounce_cap, "spp_per_step": S,
                    "kd_nodes": sd.view.num_nodes, "kd_tri_refs": sd.view.num_tris,
                    "parallelism": (f"spp-sharded x{world} + " + ("RCCL reduce" if args.dist_backend == "nccl" else
                                                                  "gloo host reduce (ranks sharing GPUs)"))
                    if world > 1 else "single GPU"},
-        "segments_per_step": seg / (args.steps * world),
-        "primary_rays_per_s": round(W * H * args.steps * world / dt, 1),
-        "roofline": {"bound": "hbm", "achieved": round(achieved, 2), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "kernel": "k_trace (KD traversal of the rays that meet the KD root box)",
-                     "k_trace_segments_per_launch": round(cand / count_seg * seg / max(1, launches), 1),
-                     "launch_grid_share": round(pt.trace_grid_share(), 4),
-                     "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
-                     "avg_launch_ms_events": round(ev_ms / max(1, ev_launches), 5),
-                     "aggregate_GBps": round(per_seg_bytes * seg / dt / 1e9, 2),
-                     "bytes_per_segment": round(per_seg_bytes, 2),
-                     "per_segment_counts": {"aabb": round(aabb / count_seg, 4), "tri": round(tri / count_seg, 4),
-                                            "hit": round(hit / count_seg, 5),
-                                            "aabb_before_k_trace": round(aabb_prep / count_seg, 4),
-                                            "k_trace_share": round(cand / count_seg, 4)}},
+        "ms_per_iteration": round(dt * 1e3 * world / iters, 4),
+        "segments_per_iteration": round(seg / iters, 1),
+        "primary_rays_per_s": round(W * H * iters / dt, 1),
+        "roofline": roof,
         "reference_980m_intersect_ms_per_iter": 79.4,
-        "intersect_ms_per_iter": round(kernel_ms / (args.steps * world), 4),
-        "roofline_note": "achieved = algorithmic bytes per k_trace launch / its average duration, as the contract "
-                         "defines it; with `pipeline` batches in flight each launch runs on launch_grid_share of the "
-                         "CUs concurrently with the others, so the chip-level algorithmic rate is aggregate_GBps "
-                         "(bytes of all segments / wall time of the timed region)",
-        "timing_note": "avg_launch_ms: k_trace launches on the device clock (s_memrealtime, first block start to "
-                       "last block end), comparable with rocprofv3 kernel-trace durations; avg_launch_ms_events: HIP "
-                       "events on the launching stream around the intersect stage (k_geoms when it runs + k_trace), "
-                       "which also count queueing behind the other in-flight iterations' kernels",
     }
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
-        # SURVEY 8(d) / BASELINE.md 3: the same oracle on one core as well (at least one whole iteration)
+        # SURVEY 8(d) / BASELINE.md 3: the same oracle on one core as well
         out["cpu_baseline_1core"] = cpu_baseline(args, threads=1, seconds=args.cpu_seconds / 2)
     pt.close()
     if dist:

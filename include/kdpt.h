@@ -176,6 +176,8 @@ typedef struct kdpt_stats {
     long long intersect_device_launches_total;
     float intersect_grid_share;  /* fraction of the persistent intersect grid one launch used in the last
                                     kdpt_trace_iterations (1 for one-at-a-time tracing) */
+    long long total_trace_rays;  /* since create/reset: rays handed to the KD traversal kernel (k_trace), i.e.
+                                    the segments whose ray meets the KD root box */
 } kdpt_stats;
 
 typedef struct kdpt_ctx kdpt_ctx;

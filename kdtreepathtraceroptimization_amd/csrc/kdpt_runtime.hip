@@ -723,7 +723,9 @@ struct ShadeArgs {
   unsigned long long* total_segments;  // running sum of paths launched into the intersect kernel
   const unsigned long long* trace_t;   // this bounce's intersect launch record (see TraceArgs)
   const unsigned long long* gspan;     // ... and the k_geoms launches' record
-  unsigned long long* trace_total;     // [2]: summed launch ticks, launches
+  unsigned long long* trace_total;     // [2]: summed launch ticks, launches (the batch's first iteration only)
+  unsigned long long* trace_rays;      // rays handed to the intersect kernel, summed (every iteration)
+  const int* ccount;                   // ... per bounce (this iteration's candidate counts)
   // next bounce's intersect-stage first part (prep_ray) for every surviving path, fused here instead of a
   // k_geoms pass: {t_min bits, (geom + 1) | walks << 16} at the path's current slot (k_scatter moves it)
   int prep_on;
@@ -816,6 +818,7 @@ __device__ inline void shade_stats(const ShadeArgs& A, int n) {
     atomicAdd(&A.trace_total[0], span);
     atomicAdd(&A.trace_total[1], 1ull);
   }
+  if (A.trace_rays) atomicAdd(A.trace_rays, (unsigned long long)A.ccount[A.depth]);
 }
 
 __device__ inline void count_prep(const ShadeArgs& A, bool tested, bool walk) {
@@ -1311,7 +1314,7 @@ struct kdpt_ctx {
   Counters last_profile{};
   unsigned long long* total_segments = nullptr;  // device running total (async use)
   unsigned long long* trace_t = nullptr;         // per-bounce intersect launch record (per slot)
-  unsigned long long* trace_total = nullptr;     // [2] device-clock intersect ticks, launches (shared)
+  unsigned long long* trace_total = nullptr;     // [3] device-clock intersect ticks, launches, rays (shared)
   double wall_khz = 100000.0;                    // s_memrealtime frequency
   int* h_counts = nullptr;  // pinned
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -2004,7 +2007,7 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     return bail(rc);
   }
   if ((rc = dalloc(c, &c->counters, 1)) || (rc = dalloc(c, &c->total_segments, 1)) ||
-      (rc = dalloc(c, &c->trace_total, 2)))
+      (rc = dalloc(c, &c->trace_total, 3)))
     return bail(rc);
   {
     int khz = 0;
@@ -2046,7 +2049,7 @@ int kdpt_reset(kdpt_ctx* c) {
   c->intersect_launches_total = 0;
   HIP_TRY(hipMemsetAsync(c->image, 0, sizeof(float) * 3 * (size_t)c->npix, c->stream));
   HIP_TRY(hipMemsetAsync(c->total_segments, 0, sizeof(unsigned long long), c->stream));
-  HIP_TRY(hipMemsetAsync(c->trace_total, 0, 2 * sizeof(unsigned long long), c->stream));
+  HIP_TRY(hipMemsetAsync(c->trace_total, 0, 3 * sizeof(unsigned long long), c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   memset(&c->stats, 0, sizeof c->stats);
   c->stats.intersect_grid_share = 1.0f;
@@ -2272,12 +2275,13 @@ int kdpt_save_hdr(kdpt_ctx* c, const char* path, float samples) {
 int kdpt_get_stats(kdpt_ctx* c, kdpt_stats* st) {
   if (!c || !st) return fail(KDPT_ERR_ARG, "null arg");
   HIP_TRY(hipSetDevice(c->device));
-  unsigned long long tot = 0, tt[2] = {0, 0};
+  unsigned long long tot = 0, tt[3] = {0, 0, 0};
   HIP_TRY(hipMemcpyAsync(&tot, c->total_segments, sizeof tot, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(tt, c->trace_total, sizeof tt, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->stats.intersect_device_ms_total = (double)tt[0] / c->wall_khz;
   c->stats.intersect_device_launches_total = (long long)tt[1];
+  c->stats.total_trace_rays = (long long)tt[2];
   c->stats.total_segments = (long long)tot;
   c->stats.intersect_ms_total = c->intersect_ms_total;
   c->stats.intersect_launches_total = c->intersect_launches_total;
@@ -2618,6 +2622,8 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       a.trace_t = c0->trace_t;
       a.gspan = c0->trace_t + 2 * c0->cap;
       a.trace_total = b == 0 ? c->trace_total : nullptr;
+      a.trace_rays = (c0->brute || c0->viz) ? nullptr : c->trace_total + 2;
+      a.ccount = c->ccount;
       a.prep_on = prep_next ? 1 : 0;
       a.prep = c->prep;
       a.tile_ccounts = c->tile_ccounts;

@@ -89,7 +89,8 @@ class Stats(C.Structure):
                 ("iterations", C.c_int), ("ms_last_iteration", C.c_float), ("ms_intersect", C.c_float),
                 ("total_segments", C.c_longlong), ("intersect_ms_total", C.c_double),
                 ("intersect_launches_total", C.c_longlong), ("intersect_device_ms_total", C.c_double),
-                ("intersect_device_launches_total", C.c_longlong), ("intersect_grid_share", C.c_float)]
+                ("intersect_device_launches_total", C.c_longlong), ("intersect_grid_share", C.c_float),
+                ("total_trace_rays", C.c_longlong)]
 
 
 class SceneDesc(C.Structure):
