@@ -69,6 +69,8 @@ def parse():
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = host-side reduce, for rehearsing the "
                          "N > 1 path with several ranks sharing one GPU")
+    ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
+                    help="kdpt_set_tuning knob for A/B runs (not for reported numbers)")
     ap.add_argument("--pmc-profile", default=None, help="profile JSON for the VALU roofline (default: "
                     "profiles/pmc_<scene>_<mesh>_<W>x<H>.json)")
     return ap.parse_args()
@@ -180,6 +182,9 @@ def main():
     opt = default_options(testing_mode=1, short_stack=0 if args.bare else 1, external_image=accum.data_ptr(),
                           bounce_cap=args.bounce_cap)
     pt = PathTracer(sd, opt, device=local)
+    for kv in args.tune:
+        name, val = kv.split("=", 1)
+        pt.set_tuning(name, float(val))
 
     def first_iter(local_iteration):  # 1-based global iteration of this rank's local iteration j (spp sharding)
         return global_iteration(local_iteration, world, rank)
@@ -269,6 +274,7 @@ def main():
                    "scene": args.scene, "mesh": args.mesh, "resolution": [W, H], "depth": args.depth,
                    "bounce_cap": args.bounce_cap, "spp_per_step": S,
                    "kd_nodes": sd.view.num_nodes, "kd_tri_refs": sd.view.num_tris,
+                   **({"tuning": args.tune} if args.tune else {}),
                    "parallelism": (f"spp-sharded x{world} + " + ("RCCL reduce" if args.dist_backend == "nccl" else
                                                                  "gloo host reduce (ranks sharing GPUs)"))
                    if world > 1 else "single GPU"},

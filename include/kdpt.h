@@ -218,6 +218,13 @@ int kdpt_hdr_encode(const float *rgb, int w, int h, uint8_t **out, size_t *len);
 int kdpt_write_hdr(const char *path, const float *rgb, int w, int h);
 void kdpt_free(void *p);
 int kdpt_get_stats(kdpt_ctx *ctx, kdpt_stats *st);
+/* Explicit A/B and diagnostic knobs (the library reads no environment variables; a context created
+ * without this call always runs the tested default route).  Names: "shade_fused" (1; 0 = k_shade +
+ * k_scan + k_scatter), "early_walk" (32) / "early_leaf" (24) (node-phase hand-over thresholds),
+ * "chunk_width0..2" (16, 64, 64), "trace_grid_frac" (grid share of every intersect launch, (0, 1]),
+ * "tree_global" (0; 1 = KD tree read from HBM/L2 instead of LDS), "profile_batches" (0),
+ * "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots (they are remade). */
+int kdpt_set_tuning(kdpt_ctx *ctx, const char *name, double value);
 int kdpt_destroy(kdpt_ctx *ctx);
 const char *kdpt_last_error(void);
 
@@ -245,6 +252,11 @@ int kdpt_wave_profile(kdpt_ctx *ctx, unsigned long long *out, int n);
 int kdpt_selftest_math(const float *x, int n, float *sin_out, float *cos_out);
 int kdpt_selftest_rng(const int *iter_idx_depth, int n, int k, float *u_out);
 int kdpt_selftest_fresnel(const float *cosines, int n, float ior, float *f_out);
+/* The glm pieces on the path (kdpt_device.h glm_kat, vendored glm 0.9.6.3 restated): fn 0
+ * intersectRayTriangle (15 floats in -> {passed, bary.xyz}; `out` holds sentinels on entry, kept where
+ * glm leaves bary unwritten), 1 normalize (3 -> 3), 2 reflect (6 -> 3), 3 refract (7 -> 3),
+ * 4 glm::rotate(quat, vec3) (7 -> 3).  Run on the device. */
+int kdpt_selftest_glm(int fn, const float *in, int n, float *out);
 /* The scatter's glibc calls as restated for gfx950 (src/interactions.h:67-83,214): fn 0 acosf(x),
  * 1 sin((double)x), 2 cos((double)x); results as doubles. */
 int kdpt_selftest_libm(int fn, const float *x, int n, double *out);

@@ -359,6 +359,30 @@ KDPT_HD void traverseKD(const DevScene& S, const Ray& ray, Hit& h, int material_
   }
 }
 
+// glm::intersectRayTriangle on (o, d) and triangle i; returns 0 = miss before the u/v
+// tests passed, 1 = passed u/v but t < 0 (bary.z still written), 2 = intersected.
+struct TriData {
+  float4 v0, e1, e2;
+};
+KDPT_HD int tri_test_v(const TriData& T, f3 o, f3 d, float& bx, float& by, float& bz) {
+  const float4 tv = T.v0, e1v = T.e1, e2v = T.e2;
+  const f3 v0 = mk3(tv.x, tv.y, tv.z), e1 = mk3(e1v.x, e1v.y, e1v.z), e2 = mk3(e2v.x, e2v.y, e2v.z);
+  const f3 p = cross(d, e2);
+  const float a = dot(e1, p);
+  if (a < FLT_EPS) return 0;
+  const float f = 1.0f / a;
+  const f3 s = sub(o, v0);
+  bx = f * dot(s, p);
+  if (bx < 0.0f) return 0;
+  if (bx > 1.0f) return 0;
+  const f3 q = cross(s, e1);
+  by = f * dot(d, q);
+  if (by < 0.0f) return 0;
+  if (by + bx > 1.0f) return 0;
+  bz = f * dot(e2, q);
+  return (bz >= 0.0f) ? 2 : 1;
+}
+
 #if defined(__HIPCC__) || defined(__HIP__)
 // ---------------------------------------------------------------------------
 // Wave-cooperative form of traverseKD for gfx950 (64-lane waves).
@@ -560,37 +584,12 @@ __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// glm::intersectRayTriangle on (o, d) and triangle i; returns 0 = miss before the u/v
-// tests passed, 1 = passed u/v but t < 0 (bary.z still written), 2 = intersected.
-struct TriData {
-  float4 v0, e1, e2;
-};
 __device__ inline TriData tri_load(const DevScene& S, int i) { return TriData{S.tv0[i], S.te1[i], S.te2[i]}; }
-
-__device__ inline int tri_test_v(const TriData& T, f3 o, f3 d, float& bx, float& by, float& bz);
 
 __device__ inline int tri_test(const DevScene& S, int i, f3 o, f3 d, float& bx, float& by, float& bz) {
   return tri_test_v(tri_load(S, i), o, d, bx, by, bz);
 }
 
-__device__ inline int tri_test_v(const TriData& T, f3 o, f3 d, float& bx, float& by, float& bz) {
-  const float4 tv = T.v0, e1v = T.e1, e2v = T.e2;
-  const f3 v0 = mk3(tv.x, tv.y, tv.z), e1 = mk3(e1v.x, e1v.y, e1v.z), e2 = mk3(e2v.x, e2v.y, e2v.z);
-  const f3 p = cross(d, e2);
-  const float a = dot(e1, p);
-  if (a < FLT_EPS) return 0;
-  const float f = 1.0f / a;
-  const f3 s = sub(o, v0);
-  bx = f * dot(s, p);
-  if (bx < 0.0f) return 0;
-  if (bx > 1.0f) return 0;
-  const f3 q = cross(s, e1);
-  by = f * dot(d, q);
-  if (by < 0.0f) return 0;
-  if (by + bx > 1.0f) return 0;
-  bz = f * dot(e2, q);
-  return (bz >= 0.0f) ? 2 : 1;
-}
 
 template <bool HYBRID>
 __device__ inline float tri_hit_t(const DevScene& S, int i, f3 o, f3 d, float bx, float by, float bz, f3& hit,
@@ -1107,6 +1106,43 @@ KDPT_HD void shade(float t, int materialId, const DevMaterial* mats, bool enable
     color = mk3(0.0f, 0.0f, 0.0f);
     bounces = 0;
   }
+}
+
+// Known answers for the glm pieces on the path, checked against the reference's vendored glm 0.9.6.3
+// (oracle/ref) on the host and on gfx950 (kdpt_selftest_glm):
+//   fn 0 intersectRayTriangle (gtx/intersect.inl:37-74) as tri_test_v runs it: in o, d, v0, v1, v2 (15
+//        floats), out {passed, bary.x, bary.y, bary.z}; bary slots the test does not reach keep the
+//        caller's values (out[1..3] are read first), which pins glm's partial writes;
+//   fn 1 normalize (3 -> 3), fn 2 reflect (I, N -> 3), fn 3 refract (I, N, eta -> 3),
+//   fn 4 glm::rotate(quat, vec3) (w, x, y, z, v -> 3).
+KDPT_HD int glm_kat_inputs(int fn) {
+  return fn == 0 ? 15 : fn == 1 ? 3 : fn == 2 ? 6 : fn == 3 ? 7 : fn == 4 ? 7 : 0;
+}
+KDPT_HD int glm_kat_outputs(int fn) { return fn == 0 ? 4 : (fn >= 1 && fn <= 4) ? 3 : 0; }
+KDPT_HD void glm_kat(int fn, const float* in, float* out) {
+  f3 r = mk3(0.0f, 0.0f, 0.0f);
+  switch (fn) {
+    case 0: {
+      const TriData T{make_float4(in[6], in[7], in[8], 0.0f),
+                      make_float4(in[9] - in[6], in[10] - in[7], in[11] - in[8], 0.0f),
+                      make_float4(in[12] - in[6], in[13] - in[7], in[14] - in[8], 0.0f)};
+      float bx = out[1], by = out[2], bz = out[3];
+      const int k = tri_test_v(T, mk3(in[0], in[1], in[2]), mk3(in[3], in[4], in[5]), bx, by, bz);
+      out[0] = k == 2 ? 1.0f : 0.0f;
+      out[1] = bx;
+      out[2] = by;
+      out[3] = bz;
+      return;
+    }
+    case 1: r = normalize(mk3(in[0], in[1], in[2])); break;
+    case 2: r = reflect(mk3(in[0], in[1], in[2]), mk3(in[3], in[4], in[5])); break;
+    case 3: r = refract(mk3(in[0], in[1], in[2]), mk3(in[3], in[4], in[5]), in[6]); break;
+    case 4: r = quat_rotate(in[0], mk3(in[1], in[2], in[3]), mk3(in[4], in[5], in[6])); break;
+    default: return;
+  }
+  out[0] = r.x;
+  out[1] = r.y;
+  out[2] = r.z;
 }
 
 }  // namespace kdpt

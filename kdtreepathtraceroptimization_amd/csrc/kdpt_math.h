@@ -76,6 +76,13 @@ KDPT_HD f3 refract(f3 I, f3 N, float eta) {
   f3 r = sub(scl(I, eta), scl(N, eta * dv + sqrtf(k)));
   return scl(r, (float)(k >= 0.0f));
 }
+// glm::rotate(quat, vec3) = quat * vec3 (gtx/quaternion.inl:153-160, gtc/quaternion.inl:319-326):
+// v + ((uv * w) + uuv) * 2 with uv = cross(q.xyz, v), uuv = cross(q.xyz, uv)
+KDPT_HD f3 quat_rotate(float w, f3 q, f3 v) {
+  const f3 uv = cross(q, v);
+  const f3 uuv = cross(q, uv);
+  return add(v, scl(add(scl(uv, w), uuv), 2.0f));
+}
 // glm::min/max (detail/func_common.inl:409-435) and std::min/max
 KDPT_HD float glm_min(float x, float y) { return x < y ? x : y; }
 KDPT_HD float glm_max(float x, float y) { return x > y ? x : y; }

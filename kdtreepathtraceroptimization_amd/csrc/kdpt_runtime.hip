@@ -136,10 +136,7 @@ __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int
   float qw = kdpt_cosf(randangle / 2.0f);
   float sh = kdpt_sinf(randangle / 2.0f);
   f3 qv = mk3(vv.x * sh, vv.y * sh, vv.z * sh);
-  // glm quat * vec3 (gtc/quaternion.inl:319-326)
-  f3 uv = cross(qv, ray.direction);
-  f3 uuv = cross(qv, uv);
-  f3 randrot = add(ray.direction, scl(add(scl(uv, qw), uuv), 2.0f));
+  const f3 randrot = quat_rotate(qw, qv, ray.direction);  // glm::rotate(Q1, direction)
   ray.origin = sub(add(ray.origin, scl(ray.direction, focalLength)), scl(randrot, focalLength));
   ray.direction = normalize(randrot);
   out.p0[index] = make_float4(ray.origin.x, ray.origin.y, ray.origin.z, 0.0f);
@@ -1258,6 +1255,11 @@ __global__ void k_selftest_rng(const int* iid, int n, int k, float* u) {
   for (int j = 0; j <= k; j++) v = u01(r);
   u[i] = v;
 }
+__global__ void k_selftest_glm(int fn, const float* in, int n, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  glm_kat(fn, in + (size_t)glm_kat_inputs(fn) * i, out + (size_t)glm_kat_outputs(fn) * i);
+}
 __global__ void k_selftest_fresnel(const float* c, int n, float R0, float* f) {
   int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -1299,7 +1301,9 @@ struct kdpt_ctx {
   unsigned long long* lb = nullptr;  // [cap][ntiles] k_shade_fused's look-back records
   int tree_mode = 0;      // TreeMode
   int trace_grid = 0;     // persistent intersect workgroups
-  bool grid_env = false;  // trace_grid fixed by KDPT_TRACE_GRID_FRAC
+  int full_trace_grid = 0;  // the occupancy-derived grid (trace_grid before a "trace_grid_frac" knob)
+  bool grid_env = false;  // trace_grid fixed by the "trace_grid_frac" tuning knob
+  bool force_global_tree = false;  // "tree_global" tuning knob: keep the tree in HBM/L2
   size_t tree_lds = 0;    // dynamic LDS bytes of the intersect kernel (TREE_LDS)
   int* tile_counts = nullptr;
   int* tile_off = nullptr;
@@ -1307,7 +1311,7 @@ struct kdpt_ctx {
   int* tile_koff = nullptr;
   int* perm = nullptr;          // trace order of the next bounce
   bool trace_order = true;      // KDPT_TRACE_ORDER=0 disables (identity order)
-  bool no_fuse = false;         // KDPT_SHADE_FUSED=0: k_shade + k_scan + k_scatter instead of k_shade_fused
+  bool no_fuse = false;         // "shade_fused" = 0: k_shade + k_scan + k_scatter instead of k_shade_fused
   bool zero_partial = false;    // k_gen_rays zeroes `image` (a pipeline slot's per-iteration partial image)
   int chunk_width[3] = {16, 64, 64};
   Counters* counters = nullptr;
@@ -1321,7 +1325,7 @@ struct kdpt_ctx {
   std::vector<hipEvent_t> bounce_ev;
   kdpt_stats stats{};
   bool count_mode = false;
-  bool sync_debug = false;  // KDPT_SYNC_DEBUG=1: synchronise and log after every launch
+  bool sync_debug = false;  // "sync_debug" = 1: synchronise and log after every launch
   // Pipelined iterations (kdpt_trace_iterations): extra slots, each a context sharing this one's
   // scene upload but owning its per-iteration buffers, stream and partial image; the partial
   // images are added into `image` in iteration order on `accum_stream`.
@@ -1331,6 +1335,7 @@ struct kdpt_ctx {
   bool profile_batches = false;
   std::vector<hipEvent_t> slot_done, slot_free;
   hipStream_t accum_stream = nullptr;
+  hipEvent_t accum_ev = nullptr;  // recorded on accum_stream; c->stream waits on it (join_accum)
   // intersect-kernel timing (testing_mode) of every iteration, read back at synchronisation
   std::vector<std::vector<hipEvent_t>> pending_ev;  // per launched iteration: 2 events per bounce
   std::vector<hipEvent_t> free_ev;
@@ -1368,6 +1373,16 @@ int dupload(kdpt_ctx* c, T** p, const T* src, size_t n) {
 int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count);
 int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, int stop_depth, bool count,
                  std::vector<hipEvent_t>* bev);
+
+// Work queued on the context's own stream that reads or writes `image` must follow the pipelined
+// accumulation (kdpt_trace_iterations adds partial images on accum_stream without a host sync).
+int join_accum(kdpt_ctx* c) {
+  if (!c->accum_stream) return KDPT_OK;
+  if (!c->accum_ev) HIP_TRY(hipEventCreateWithFlags(&c->accum_ev, hipEventDisableTiming));
+  HIP_TRY(hipEventRecord(c->accum_ev, c->accum_stream));
+  HIP_TRY(hipStreamWaitEvent(c->stream, c->accum_ev, 0));
+  return KDPT_OK;
+}
 
 // stats.segments / seg_per_bounce / bounces of the iteration whose counts are in h_counts
 int segments_from_counts(kdpt_ctx* c) {
@@ -1629,9 +1644,7 @@ int setup_trace(kdpt_ctx* c) {
   const size_t static_lds = sizeof(WaveLeafLDS) * (TRACE_BLOCK / 64);
   const size_t tree_bytes = 32 * (size_t)c->S.num_nodes + 32 * (size_t)c->S.num_clusters;  // + cluster boxes
   const size_t lds_max = prop.sharedMemPerBlock > 0 ? prop.sharedMemPerBlock : 65536;
-  const char* tm = getenv("KDPT_TREE");  // "global": keep the tree in HBM/L2 (experiments)
-  const bool force_global = tm && strcmp(tm, "global") == 0;
-  if (c->S.pnodes && static_lds + tree_bytes <= lds_max && !force_global) {
+  if (c->S.pnodes && static_lds + tree_bytes <= lds_max && !c->force_global_tree) {
     c->tree_mode = TREE_LDS;
     c->tree_lds = tree_bytes;
   }
@@ -1660,13 +1673,7 @@ int setup_trace(kdpt_ctx* c) {
   if (rc) return rc;
   if (blocks < 1) return fail(KDPT_ERR_UNSUPPORTED, "intersect kernel does not fit on a CU");
   c->trace_grid = blocks * prop.multiProcessorCount;
-  if (const char* gf = getenv("KDPT_TRACE_GRID_FRAC")) {  // experiment: a fixed fraction of the grid
-    const double f = atof(gf);
-    if (f > 0.0 && f <= 1.0) {
-      c->trace_grid = std::max(1, (int)(c->trace_grid * f));
-      c->grid_env = true;
-    }
-  }
+  c->full_trace_grid = c->trace_grid;
   return KDPT_OK;
 }
 
@@ -2014,28 +2021,65 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, device) == hipSuccess && khz > 0)
       c->wall_khz = khz;
   }
-  {
-    const char* e = getenv("KDPT_SYNC_DEBUG");
-    c->sync_debug = e && e[0] == '1';
-    const char* t = getenv("KDPT_TRACE_ORDER");
-    c->S.trace_mode = t ? atoi(t) : 0;
-    // leave the node phase early once at most 32 lanes still walk and at least 24 wait on a leaf (the
-    // walkers resume after the leaf phase; A/B over the bench: 3 390 -> 3 540 Mrays/s; "0,65" = never)
-    c->S.early_walk = 32;
-    c->S.early_leaf = 24;
-    const char* ew = getenv("KDPT_EARLY_LEAF");  // "walkers,leaves", e.g. "8,16"
-    if (ew) sscanf(ew, "%d,%d", &c->S.early_walk, &c->S.early_leaf);
-    const char* cw = getenv("KDPT_CHUNK_WIDTHS");  // e.g. "16,32,64"
-    if (cw) sscanf(cw, "%d,%d,%d", &c->chunk_width[0], &c->chunk_width[1], &c->chunk_width[2]);
-    for (int k = 0; k < 3; k++) c->chunk_width[k] = std::min(64, std::max(1, c->chunk_width[k]));
-    c->trace_order = false;  // superseded by k_geoms' candidate lists (KDPT_TRACE_ORDER is ignored)
-    if (const char* f = getenv("KDPT_SHADE_FUSED")) c->no_fuse = f[0] == '0';
-  }
+  // The product reads no environment variables: every route is the tested default unless a caller
+  // changes it explicitly with kdpt_set_tuning (A/B experiments, the three-kernel compaction test).
+  c->S.trace_mode = 0;
+  // leave the node phase early once at most 32 lanes still walk and at least 24 wait on a leaf (the
+  // walkers resume after the leaf phase; A/B over the bench: 3 390 -> 3 540 Mrays/s; 0 / 65 = never)
+  c->S.early_walk = 32;
+  c->S.early_leaf = 24;
+  c->trace_order = false;  // superseded by k_geoms' candidate lists
   if ((rc = setup_trace(c))) return bail(rc);
   c->S.trip_limit = 8 * std::max(c->S.num_nodes, 1) + 64;
   if ((rc = alloc_iteration_events(c))) return bail(rc);
   if ((rc = kdpt_reset(c))) return bail(rc);
   *out = c;
+  return KDPT_OK;
+}
+
+int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
+  if (!c || !name) return fail(KDPT_ERR_ARG, "null arg");
+  if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
+  HIP_TRY(hipSetDevice(c->device));
+  // pipeline slots copy the knobs when they are made: drop them so the next kdpt_trace_iterations
+  // makes new ones
+  if (!c->slots.empty()) {
+    int rc = kdpt_synchronize(c);
+    if (rc) return rc;
+    for (auto sl : c->slots) kdpt_destroy(sl);
+    for (auto e : c->slot_done) (void)hipEventDestroy(e);
+    for (auto e : c->slot_free) (void)hipEventDestroy(e);
+    c->slots.clear();
+    c->slot_done.clear();
+    c->slot_free.clear();
+  }
+  const std::string k(name);
+  const int v = (int)value;
+  if (k == "shade_fused") {
+    c->no_fuse = v == 0;
+  } else if (k == "early_walk") {
+    c->S.early_walk = v;
+  } else if (k == "early_leaf") {
+    c->S.early_leaf = v;
+  } else if (k == "chunk_width0" || k == "chunk_width1" || k == "chunk_width2") {
+    c->chunk_width[k.back() - '0'] = std::min(64, std::max(1, v));
+  } else if (k == "trace_grid_frac") {
+    if (!(value > 0.0 && value <= 1.0)) return fail(KDPT_ERR_ARG, "trace_grid_frac must be in (0, 1]");
+    c->trace_grid = std::max(1, (int)(c->full_trace_grid * value));
+    c->grid_env = value < 1.0;
+  } else if (k == "tree_global") {
+    c->force_global_tree = v != 0;
+    const double frac = (double)c->trace_grid / std::max(1, c->full_trace_grid);
+    int rc = setup_trace(c);
+    if (rc) return rc;
+    if (c->grid_env) c->trace_grid = std::max(1, (int)(c->full_trace_grid * frac));
+  } else if (k == "profile_batches") {
+    c->profile_batches = v != 0;
+  } else if (k == "sync_debug") {
+    c->sync_debug = v != 0;
+  } else {
+    return fail(KDPT_ERR_ARG, "unknown tuning knob " + k);
+  }
   return KDPT_OK;
 }
 
@@ -2156,11 +2200,8 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
   for (auto sl : c->slots)
     sl->trace_grid = c->grid_env ? c->trace_grid : std::max(1, c->trace_grid * 2 / std::max(2, depth));
   c->stats.intersect_grid_share = c->slots.empty() ? 1.0f : (float)c->slots[0]->trace_grid / (float)c->trace_grid;
-  {  // diagnostic: KDPT_PROFILE_BATCHES=1 runs the counting intersect kernel (kdpt_wave_profile after sync)
-    const char* e = getenv("KDPT_PROFILE_BATCHES");
-    c->profile_batches = e && e[0] == '1';
-    if (c->profile_batches) HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(Counters), c->stream));
-  }
+  // diagnostic ("profile_batches" knob): the counting intersect kernel (kdpt_wave_profile after sync)
+  if (c->profile_batches) HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(Counters), c->stream));
   for (int kb = 0, bi = 0; kb < count; kb += B, bi++) {
     const int nb = std::min(B, count - kb);
     const int g = bi % ngroups;
@@ -2215,6 +2256,8 @@ int kdpt_write_pbo(kdpt_ctx* c, int iter, uint8_t* rgba) {
   if (!c || !rgba || iter == 0) return fail(KDPT_ERR_ARG, "bad arg");
   HIP_TRY(hipSetDevice(c->device));
   uchar4* d = nullptr;
+  int rc = join_accum(c);
+  if (rc) return rc;
   HIP_TRY(hipMalloc((void**)&d, sizeof(uchar4) * (size_t)c->npix));
   hipLaunchKernelGGL(k_pbo, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->image, c->npix, iter, d);
   HIP_TRY(hipGetLastError());
@@ -2307,6 +2350,7 @@ int kdpt_destroy(kdpt_ctx* c) {
     for (auto e : evs) (void)hipEventDestroy(e);
   for (auto e : c->free_ev) (void)hipEventDestroy(e);
   if (c->accum_stream) (void)hipStreamDestroy(c->accum_stream);
+  if (c->accum_ev) (void)hipEventDestroy(c->accum_ev);
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->h_counts) (void)hipHostFree(c->h_counts);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
@@ -2456,6 +2500,22 @@ int kdpt_selftest_rng(const int* iid, int n, int k, float* u) {
   HIP_TRY(hipGetLastError());
   HIP_TRY(hipMemcpy(u, du, sizeof(float) * n, hipMemcpyDeviceToHost));
   (void)hipFree(di); (void)hipFree(du);
+  return KDPT_OK;
+}
+
+int kdpt_selftest_glm(int fn, const float* in, int n, float* out) {
+  const int ni = glm_kat_inputs(fn), no = glm_kat_outputs(fn);
+  if (!ni || n < 0 || (n && (!in || !out))) return fail(KDPT_ERR_ARG, "bad glm selftest arguments");
+  if (!n) return KDPT_OK;
+  float *din, *dout;
+  HIP_TRY(hipMalloc((void**)&din, sizeof(float) * ni * (size_t)n));
+  HIP_TRY(hipMalloc((void**)&dout, sizeof(float) * no * (size_t)n));
+  HIP_TRY(hipMemcpy(din, in, sizeof(float) * ni * (size_t)n, hipMemcpyHostToDevice));
+  HIP_TRY(hipMemcpy(dout, out, sizeof(float) * no * (size_t)n, hipMemcpyHostToDevice));  // sentinels
+  hipLaunchKernelGGL(k_selftest_glm, dim3((n + 255) / 256), dim3(256), 0, 0, fn, din, n, dout);
+  HIP_TRY(hipGetLastError());
+  HIP_TRY(hipMemcpy(out, dout, sizeof(float) * no * (size_t)n, hipMemcpyDeviceToHost));
+  (void)hipFree(din); (void)hipFree(dout);
   return KDPT_OK;
 }
 
@@ -2687,6 +2747,8 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
 }
 
 int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
+  int rc = join_accum(c);
+  if (rc) return rc;
   return launch_batch(&c, &iter, 1, c->stream, stop_depth, count, c->rec_ev ? c->rec_ev : &c->bounce_ev);
 }
 

@@ -112,7 +112,7 @@ EXPORTS = [
     "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_count_split", "kdpt_wave_profile", "kdpt_selftest_math", "kdpt_selftest_rng",
     "kdpt_selftest_fresnel", "kdpt_selftest_libm", "kdpt_selftest_libm_digest", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
     "kdpt_save_rgb8", "kdpt_save_png", "kdpt_save_hdr", "kdpt_png_encode", "kdpt_write_png", "kdpt_hdr_encode",
-    "kdpt_write_hdr", "kdpt_free",
+    "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm",
 ]
 
 _lib = None
@@ -170,6 +170,10 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_write_hdr.argtypes = [C.c_char_p, P(C.c_float), C.c_int, C.c_int]
     lib.kdpt_free.argtypes = [C.c_void_p]
     lib.kdpt_free.restype = None
+    if hasattr(lib, "kdpt_selftest_glm"):
+        lib.kdpt_selftest_glm.argtypes = [C.c_int, P(C.c_float), C.c_int, P(C.c_float)]
+    if hasattr(lib, "kdpt_set_tuning"):  # absent from older builds used in A/B runs
+        lib.kdpt_set_tuning.argtypes = [C.c_void_p, C.c_char_p, C.c_double]
     _lib = lib
     return lib
 
@@ -385,6 +389,10 @@ class PathTracer:
         _check(self.lib.kdpt_write_pbo(self._ctx, int(iteration), out.ctypes.data_as(C.POINTER(C.c_uint8))),
                "kdpt_write_pbo")
         return out
+
+    def set_tuning(self, name: str, value: float):
+        """kdpt_set_tuning: an explicit A/B or diagnostic knob (the library reads no environment)."""
+        _check(self.lib.kdpt_set_tuning(self._ctx, name.encode(), float(value)), f"kdpt_set_tuning({name})")
 
     def reset(self):
         _check(self.lib.kdpt_reset(self._ctx), "kdpt_reset")

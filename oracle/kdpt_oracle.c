@@ -2026,3 +2026,47 @@ void orc_save_image(const float *image, int W, int H, float samples, unsigned ch
             }
         }
 }
+
+/* Known answers of the glm pieces (vendored glm 0.9.6.3; kdpt_selftest_glm's numbering):
+ * fn 0 intersectRayTriangle (o, d, v0, v1, v2 -> passed, bary.xyz; out[1..3] hold the caller's
+ * sentinels, kept where glm does not write), 1 normalize, 2 reflect, 3 refract, 4 glm::rotate(quat, v). */
+void orc_glm_array(int fn, const float *in, int n, float *out) {
+    const int ni = fn == 0 ? 15 : fn == 1 ? 3 : fn == 2 ? 6 : 7, no = fn == 0 ? 4 : 3;
+    for (int i = 0; i < n; i++) {
+        const float *a = in + (size_t)ni * i;
+        float *o = out + (size_t)no * i;
+        v3 r = V3(0.0f, 0.0f, 0.0f);
+        if (fn == 0) {
+            v3 bary = V3(o[1], o[2], o[3]);
+            int hit = intersectRayTriangle(V3(a[0], a[1], a[2]), V3(a[3], a[4], a[5]), V3(a[6], a[7], a[8]),
+                                           V3(a[9], a[10], a[11]), V3(a[12], a[13], a[14]), &bary);
+            o[0] = hit ? 1.0f : 0.0f;
+            o[1] = bary.x; o[2] = bary.y; o[3] = bary.z;
+            continue;
+        } else if (fn == 1) {
+            r = vnormalize(V3(a[0], a[1], a[2]));
+        } else if (fn == 2) {
+            r = glm_reflect(V3(a[0], a[1], a[2]), V3(a[3], a[4], a[5]));
+        } else if (fn == 3) {
+            r = glm_refract(V3(a[0], a[1], a[2]), V3(a[3], a[4], a[5]), a[6]);
+        } else if (fn == 4) { /* q * v, gtc/quaternion.inl:319-326 */
+            v3 q = V3(a[1], a[2], a[3]), v = V3(a[4], a[5], a[6]);
+            v3 uv = vcross(q, v), uuv = vcross(q, uv);
+            r = vadd(v, vscale(vadd(vscale(uv, a[0]), uuv), 2.0f));
+        }
+        o[0] = r.x; o[1] = r.y; o[2] = r.z;
+    }
+}
+
+/* Geom matrices (src/scene.cpp:165-168): buildTransformationMatrix (src/utilities.cpp:65-72),
+ * glm::inverse, glm::inverseTranspose of n translation/rotation/scale triples -> 48 floats each. */
+void orc_geom_matrices(const float *trs, int n, float *out) {
+    for (int i = 0; i < n; i++) {
+        const float *t = trs + 9 * (size_t)i;
+        m4 tr = buildTransformationMatrix(V3(t[0], t[1], t[2]), V3(t[3], t[4], t[5]), V3(t[6], t[7], t[8]));
+        m4 inv = m4inverse(&tr), it = m4inverseTranspose(&tr);
+        memcpy(out + 48 * (size_t)i, &tr, 64);
+        memcpy(out + 48 * (size_t)i + 16, &inv, 64);
+        memcpy(out + 48 * (size_t)i + 32, &it, 64);
+    }
+}

@@ -235,6 +235,11 @@ void orc_libm_array(int fn, const float *x, int n, double *out);
 /* order-independent digest of fn over the float bit patterns first .. first+count-1:
    sum of splitmix64(result bits ^ splitmix64(input bits)) (kdpt_selftest_libm_digest computes the same) */
 uint64_t orc_libm_digest(int fn, uint32_t first, uint64_t count);
+/* glm known answers (kdpt_selftest_glm's numbering): 0 intersectRayTriangle, 1 normalize, 2 reflect,
+ * 3 refract, 4 glm::rotate(quat, vec3); out[1..3] of fn 0 hold sentinels on entry */
+void orc_glm_array(int fn, const float *in, int n, float *out);
+/* Geom matrices: transform, inverse, invTranspose (48 floats) per translation/rotation/scale triple */
+void orc_geom_matrices(const float *trs, int n, float *out);
 /* getFresnelVal with dot(N,-I) == cosines[i] */
 void orc_fresnel_array(const float *cosines, int n, float ior, float *f);
 

@@ -107,6 +107,8 @@ def lib():
         L.orc_fresnel_array.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
         L.orc_trace_ray.argtypes = [P(OScene), P(C.c_float), P(C.c_float), C.c_int, P(C.c_double)]
         L.orc_save_image.argtypes = [P(C.c_float), C.c_int, C.c_int, C.c_float, P(C.c_uint8), P(C.c_float)]
+        L.orc_glm_array.argtypes = [C.c_int, P(C.c_float), C.c_int, P(C.c_float)]
+        L.orc_geom_matrices.argtypes = [P(C.c_float), C.c_int, P(C.c_float)]
         _lib = L
     return _lib
 
@@ -296,3 +298,20 @@ def save_image(image: np.ndarray, samples: float):
     lib().orc_save_image(_fp(image), w, h, float(np.float32(samples)), rgb.ctypes.data_as(C.POINTER(C.c_uint8)),
                          _fp(lin))
     return rgb, lin
+
+
+def glm_array(fn: int, x: np.ndarray, out: np.ndarray) -> np.ndarray:
+    """orc_glm_array: the oracle's glm restatements (kdpt_selftest_glm numbering); `out` holds the
+    sentinels on entry and is updated in place."""
+    x = np.ascontiguousarray(x, np.float32)
+    assert out.dtype == np.float32 and out.flags.c_contiguous
+    lib().orc_glm_array(fn, _fp(x), len(x), _fp(out))
+    return out
+
+
+def geom_matrices(trs: np.ndarray) -> np.ndarray:
+    """transform, inverseTransform, invTranspose (48 floats) per translation/rotation/scale triple."""
+    trs = np.ascontiguousarray(trs, np.float32).reshape(-1, 9)
+    out = np.empty((len(trs), 48), np.float32)
+    lib().orc_geom_matrices(_fp(trs), len(trs), _fp(out))
+    return out

@@ -171,15 +171,15 @@ def test_path_state_after_each_bounce(kdpt, oracle, stop_depth):
 
 
 @pytest.mark.parametrize("res", [(96, 96), (800, 800)])
-def test_fused_shading_equals_scan_scatter(kdpt, oracle, monkeypatch, res):
+def test_fused_shading_equals_scan_scatter(kdpt, oracle, res):
     """k_shade_fused (single-pass decoupled look-back compaction) and k_shade + k_scan + k_scatter
-    (KDPT_SHADE_FUSED=0) give the same images and path arrays; the small size also against the oracle.
+    (kdpt_set_tuning "shade_fused" = 0) give the same images and path arrays; the small size also against the oracle.
     800x800 has 2500 tiles per bounce, so most tiles find their offset through other tiles' counts."""
     desc = load_fixture_scene("cornell", "dragon_5", res=res, depth=8)
     out = {}
     for fused in ("1", "0"):
-        monkeypatch.setenv("KDPT_SHADE_FUSED", fused)
         with _pt(kdpt, desc) as pt:
+            pt.set_tuning("shade_fused", int(fused))
             paths = pt.debug_paths(3, 2)
             pt.reset()
             for it in (1, 3, 4):
@@ -264,3 +264,44 @@ def test_pipelined_iterations_bit_exact(kdpt, pipeline, batch):
     pip.close()
     assert tot_pip == tot_seq
     assert np.array_equal(img_pip.view(np.uint32), img_seq.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_entry_points_order_after_pipelined_accumulation(kdpt):
+    """kdpt_trace_iterations returns with partial images still being added on its accumulation stream;
+    a following kdpt_trace_iteration (gather into the image on the context's stream) and kdpt_write_pbo
+    must see every earlier addition without an explicit kdpt_synchronize in between."""
+    desc = load_fixture_scene("cornell", "dragon_5", res=(96, 80), depth=8)
+    sd = kdpt.SceneData.from_description(desc)
+    with kdpt.PathTracer(sd, kdpt.default_options()) as seq:
+        for it in range(1, 18):
+            seq.trace_iteration(it)
+        img_seq, pbo_seq = seq.image(), seq.pbo(17)
+    with kdpt.PathTracer(sd, kdpt.default_options()) as pip:
+        pip.trace_iterations(1, 16, pipeline=4, batch=4)
+        pip.trace_iteration(17)  # no synchronize before it
+        pbo = pip.pbo(17)
+        img = pip.image()
+    assert np.array_equal(img.view(np.uint32), img_seq.view(np.uint32))
+    assert np.array_equal(pbo, pbo_seq)
+
+
+@pytest.mark.gpu
+def test_tuning_knobs_keep_parity(kdpt):
+    """Every kdpt_set_tuning route gives the default route's bits (the knobs change scheduling only);
+    unknown names are refused."""
+    desc = load_fixture_scene("cornell", "dragon_5", res=(96, 80), depth=8)
+    sd = kdpt.SceneData.from_description(desc)
+    with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
+        pt.trace_iterations(1, 8, pipeline=2, batch=4)
+        pt.synchronize()
+        ref = pt.image().copy()
+        with pytest.raises(kdpt.KdptError):
+            pt.set_tuning("no_such_knob", 1)
+    for name, val in (("tree_global", 1), ("early_walk", 0), ("early_leaf", 65), ("chunk_width0", 64),
+                      ("chunk_width1", 8), ("trace_grid_frac", 0.1), ("shade_fused", 0)):
+        with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
+            pt.set_tuning(name, val)
+            pt.trace_iterations(1, 8, pipeline=2, batch=4)
+            pt.synchronize()
+            assert np.array_equal(pt.image().view(np.uint32), ref.view(np.uint32)), name

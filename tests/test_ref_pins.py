@@ -1,0 +1,180 @@
+"""Parity pins from the reference's own code (tests/golden/ref_pins.json, made by
+tests/golden/make_ref_pins.py from oracle/_ref/ref_pins = the reference's src/image.cpp + src/stb.cpp +
+src/utilities.cpp and its vendored glm 0.9.6.3, compiled in place from /root/reference):
+
+- the glm pieces on the path (intersectRayTriangle incl. its partial bary writes, normalize, reflect,
+  refract, glm::rotate(quat, vec3)) on 2^20 seeded inputs each: the oracle, the product's device source
+  compiled for the host, and (-m gpu) the gfx950 code give the reference's bits;
+- the Geom matrices (buildTransformationMatrix, glm::inverse, glm::inverseTranspose, src/scene.cpp:
+  165-168): the oracle and the product's host scene builder give the reference's bits for every scene
+  geom and 20 000 random triples;
+- image::savePNG / image::saveHDR (src/image.cpp:22-45 over stb_image_write): the product's encoders
+  give the reference's bytes for seeded images and for an oracle render; (-m gpu) kdpt_save_png /
+  kdpt_save_hdr of the GPU render of the same scene write the reference's file bytes.
+
+Where /root/reference exists the digests are recomputed from the reference binary as well, so the
+fixture itself stays pinned.  The bounce as a whole stays pinned only by the survey's anchor runs
+(reference kernels run host-side during the survey) and the oracle restatement.
+"""
+import hashlib
+import json
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+import pytest
+
+import kat_inputs as K
+import sys
+sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden"))
+from conftest import HAS_REFERENCE, ROOT, TESTS
+
+PINS = json.load(open(os.path.join(TESTS, "golden", "ref_pins.json")))
+REF_PINS = os.path.join(ROOT, "oracle", "_ref", "ref_pins")
+has_ref_bin = pytest.mark.skipif(not (HAS_REFERENCE and os.path.exists(REF_PINS)),
+                                 reason="reference sources / oracle/_ref/ref_pins not present")
+
+
+@pytest.fixture(scope="module")
+def glm_host():
+    exe = os.path.join(ROOT, "build", "glm_host")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-I",
+                    os.path.join(ROOT, "include"), os.path.join(TESTS, "native", "glm_host.cpp"), "-o", exe],
+                   check=True)
+    return exe
+
+
+def _glm_host(exe, fn, x):
+    out = K.glm_sentinels(fn, len(x))
+    with tempfile.TemporaryDirectory() as tmp:
+        xin, xout = os.path.join(tmp, "in.f32"), os.path.join(tmp, "out.f32")
+        x.tofile(xin)
+        out.tofile(xout)
+        subprocess.run([exe, str(fn), str(len(x)), xin, xout], check=True, timeout=300)
+        return np.fromfile(xout, np.float32).reshape(out.shape)
+
+
+@pytest.mark.parametrize("fn", sorted(K.GLM_FNS))
+def test_glm_oracle_and_host_device_source_equal_reference(oracle, glm_host, fn):
+    x = K.glm_inputs(fn)
+    want = PINS["glm"][str(fn)]["sha256"]
+    orc = oracle.glm_array(fn, x, K.glm_sentinels(fn, len(x)))
+    assert K.sha256(orc) == want, "oracle"
+    host = _glm_host(glm_host, fn, x)
+    assert K.sha256(host) == want, "kdpt_device.h glm_kat compiled for the host"
+
+
+def test_glm_triangle_inputs_cover_every_exit():
+    rec = PINS["glm"]["0"]
+    n = rec["n"]
+    assert 0.02 * n < rec["hits"] < 0.5 * n
+    ux, uy, uz = rec["bary_unwritten"]
+    # det < eps leaves all three unwritten; u out of range leaves y, z; v out of range leaves z;
+    # t < 0 writes all three but misses
+    assert 0 < ux < uy < uz < n - rec["hits"]
+
+
+@has_ref_bin
+@pytest.mark.parametrize("fn", sorted(K.GLM_FNS))
+def test_glm_fixture_matches_reference_binary(fn):
+    import make_ref_pins as M
+    with tempfile.TemporaryDirectory() as tmp:
+        out = M.ref_glm(fn, K.glm_inputs(fn), tmp)
+    assert K.sha256(out) == PINS["glm"][str(fn)]["sha256"]
+
+
+def _product_geom_matrices(kdpt, trs):
+    """The product's host scene builder (kdpt_scene_build) on one geom per triple."""
+    from kdtreepathtraceroptimization_amd import load_fixture_scene
+    desc = load_fixture_scene("cornell")
+    desc.geom_type = np.ones(len(trs), np.int32)
+    desc.geom_material = np.zeros(len(trs), np.int32)
+    desc.geom_trs = np.ascontiguousarray(trs, np.float32)
+    sd = kdpt.SceneData.from_description(desc)
+    g = np.frombuffer(sd.geoms_bytes(), np.uint8).reshape(len(trs), 236)
+    m = g[:, 44:236].copy().view(np.float32).reshape(len(trs), 48)
+    sd.close()
+    return m
+
+
+def test_geom_matrices_equal_reference(oracle, kdpt):
+    import make_ref_pins as M
+    trs = M.all_trs()
+    assert len(trs) == PINS["geom"]["n"]
+    assert K.sha256(oracle.geom_matrices(trs)) == PINS["geom"]["sha256"], "oracle"
+    assert K.sha256(_product_geom_matrices(kdpt, trs)) == PINS["geom"]["sha256"], "product host builder"
+
+
+@has_ref_bin
+def test_geom_fixture_matches_reference_binary():
+    import make_ref_pins as M
+    with tempfile.TemporaryDirectory() as tmp:
+        m = M.ref_geom(M.all_trs(), tmp)
+    assert K.sha256(m) == PINS["geom"]["sha256"]
+
+
+def _rgb8(im):
+    """image::savePNG's bytes: glm::clamp(pixel, 0, 1) * 255.f, (unsigned char) (src/image.cpp:27-31)."""
+    return (np.minimum(np.maximum(im, np.float32(0)), np.float32(1)) * np.float32(255)).astype(np.uint8)
+
+
+def test_png_hdr_encoders_equal_reference_writer(kdpt):
+    import make_ref_pins as M
+    for name, im in M.pin_images():
+        rec = PINS["images"][name]
+        assert list(im.shape) == rec["shape"]
+        png = kdpt.png_encode(_rgb8(im))
+        hdr = kdpt.hdr_encode(np.ascontiguousarray(im, np.float32))
+        assert hashlib.sha256(png).hexdigest() == rec["png_sha256"], name
+        assert hashlib.sha256(hdr).hexdigest() == rec["hdr_sha256"], name
+
+
+def test_oracle_save_image_bytes_are_savepng_conversion(oracle):
+    """The oracle's saveImage bytes are what image::savePNG computes from saveImage's pixels."""
+    import make_ref_pins as M
+    from kdtreepathtraceroptimization_amd import load_fixture_scene
+    desc = load_fixture_scene("cornell", "sphere_low_1", res=(64, 64), depth=8)
+    img, _ = oracle.OracleScene.from_description(desc).render(1, 4)
+    rgb, lin = oracle.save_image(img, 4.0)
+    assert np.array_equal(lin.view(np.uint32), M.render_image().view(np.uint32))
+    assert np.array_equal(rgb, _rgb8(lin))
+
+
+@has_ref_bin
+def test_image_fixture_matches_reference_binary():
+    import make_ref_pins as M
+    with tempfile.TemporaryDirectory() as tmp:
+        for name, im in M.pin_images():
+            png, hdr = M.ref_image_files(im, tmp)
+            assert hashlib.sha256(png).hexdigest() == PINS["images"][name]["png_sha256"], name
+            assert hashlib.sha256(hdr).hexdigest() == PINS["images"][name]["hdr_sha256"], name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fn", sorted(K.GLM_FNS))
+def test_device_glm_equals_reference(kdpt, fn):
+    import ctypes as C
+    x = K.glm_inputs(fn)
+    out = K.glm_sentinels(fn, len(x))
+    P = C.POINTER(C.c_float)
+    rc = kdpt.load_library().kdpt_selftest_glm(fn, x.ctypes.data_as(P), len(x), out.ctypes.data_as(P))
+    assert rc == 0
+    assert K.sha256(out) == PINS["glm"][str(fn)]["sha256"]
+
+
+@pytest.mark.gpu
+def test_gpu_saved_png_hdr_equal_reference_writer(kdpt, tmp_path):
+    """kdpt_save_png / kdpt_save_hdr of the GPU render write the files the reference's saveImage +
+    image::savePNG / saveHDR write for the same render."""
+    from kdtreepathtraceroptimization_amd import load_fixture_scene
+    desc = load_fixture_scene("cornell", "sphere_low_1", res=(64, 64), depth=8)
+    rec = PINS["images"]["render_cornell_sphere_low_1_64x64_4spp"]
+    with kdpt.PathTracer(kdpt.SceneData.from_description(desc)) as pt:
+        for it in range(1, 5):
+            pt.trace_iteration(it)
+        pt.save_png(str(tmp_path / "r.png"), 4.0)
+        pt.save_hdr(str(tmp_path / "r.hdr"), 4.0)
+    assert hashlib.sha256((tmp_path / "r.png").read_bytes()).hexdigest() == rec["png_sha256"]
+    assert hashlib.sha256((tmp_path / "r.hdr").read_bytes()).hexdigest() == rec["hdr_sha256"]

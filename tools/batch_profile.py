@@ -1,9 +1,8 @@
-"""Wave profile of the intersect kernel under kdpt_trace_iterations (KDPT_PROFILE_BATCHES=1)."""
+"""Wave profile of the intersect kernel under kdpt_trace_iterations (tuning knob "profile_batches")."""
 import json
 import os
 import sys
 
-os.environ["KDPT_PROFILE_BATCHES"] = "1"
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 8:
     os.environ["GPU_MAX_HW_QUEUES"] = "8"
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
@@ -15,6 +14,7 @@ sd = SceneData.from_description(load_fixture_scene("cornell", sys.argv[1] if len
 for cfg in (sys.argv[2] if len(sys.argv) > 2 else "1x1,2x2,1x4").split(","):
     p, b = (int(v) for v in cfg.split("x"))
     pt = PathTracer(sd, default_options(testing_mode=1))
+    pt.set_tuning("profile_batches", 1)
     pt.trace_iterations(1, 4 * p * b, pipeline=p, batch=b)
     pt.synchronize()
     prof = pt.wave_profile()
