@@ -89,7 +89,9 @@ def main():
         for fn, name in K.GLM_FNS.items():
             x = K.glm_inputs(fn)
             out = ref_glm(fn, x, tmp)
-            rec = {"name": name, "n": len(x), "sha256": K.sha256(out)}
+            gen_nan = np.isnan(out) & (out.view(np.uint32) != K.SENTINEL_BITS)
+            rec = {"name": name, "n": len(x), "sha256": K.sha256(out), "nan_values": int(gen_nan.sum()),
+                   "sha256_nan_canonical": K.sha256_nan_canonical(out)}
             if fn == 0:
                 bits = out.view(np.uint32)
                 rec["hits"] = int((out[:, 0] == 1.0).sum())

@@ -93,3 +93,11 @@ def images(seed: int = 3):
 
 def sha256(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
+
+
+def sha256_nan_canonical(a: np.ndarray) -> str:
+    """sha256 with every NaN replaced by one bit pattern: IEEE 754 leaves a generated NaN's sign and
+    payload open (x86 SSE makes 0xffc00000, gfx950 0x7fc00000); NaN positions still count."""
+    b = np.ascontiguousarray(a, np.float32).copy()
+    b.view(np.uint32)[np.isnan(b)] = np.uint32(0x7FC00000)
+    return sha256(b)

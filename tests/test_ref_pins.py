@@ -66,6 +66,15 @@ def test_glm_oracle_and_host_device_source_equal_reference(oracle, glm_host, fn)
     assert K.sha256(host) == want, "kdpt_device.h glm_kat compiled for the host"
 
 
+def test_glm_nan_values_only_where_glm_makes_them():
+    """NaNs arise only in normalize (zero vectors: 0 * inf) and refract (total internal reflection:
+    sqrt(k < 0) * 0).  The reference's scatterRay tests refract's condition first (in double,
+    src/interactions.h:248-250) and reflects instead, so a NaN direction there can only arise at the
+    float/double boundary of that test."""
+    assert {fn: PINS["glm"][str(fn)]["nan_values"] > 0 for fn in K.GLM_FNS} == {0: False, 1: True, 2: False,
+                                                                               3: True, 4: False}
+
+
 def test_glm_triangle_inputs_cover_every_exit():
     rec = PINS["glm"]["0"]
     n = rec["n"]
@@ -161,7 +170,12 @@ def test_device_glm_equals_reference(kdpt, fn):
     P = C.POINTER(C.c_float)
     rc = kdpt.load_library().kdpt_selftest_glm(fn, x.ctypes.data_as(P), len(x), out.ctypes.data_as(P))
     assert rc == 0
-    assert K.sha256(out) == PINS["glm"][str(fn)]["sha256"]
+    rec = PINS["glm"][str(fn)]
+    # bit-exact, except that a NaN the arithmetic generates (refract's sqrt of a negative k, glm's
+    # `* (k >= 0)` keeping it) may carry gfx950's sign instead of x86's: same NaN positions
+    assert K.sha256_nan_canonical(out) == rec["sha256_nan_canonical"]
+    if fn != 3:
+        assert K.sha256(out) == rec["sha256"]
 
 
 @pytest.mark.gpu
