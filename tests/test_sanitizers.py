@@ -1,0 +1,112 @@
+"""The CPU side under AddressSanitizer + UndefinedBehaviorSanitizer (run the CPU
+restatement under ASan/UBSan; the product's host code parses untrusted OBJ/MTL/scene text).
+
+- tests/native/asan_host.cpp + the product's csrc/scene_host.cpp + csrc/image_io.cpp + the traversal of
+  csrc/kdpt_device.h compiled for the host, all sanitized, over the edge OBJs of test_host_builder.py,
+  malformed OBJ and scene files (missing/short normal lists, out-of-range, zero and negative indices,
+  truncated faces, garbage, NaN/inf coordinates, a 200 kB line, a missing mtllib) and, where present,
+  the reference's own meshes: each input is either built or refused with an error code, never a
+  sanitizer report;
+- tests/native/traverse_diff.cpp linked with a sanitized build of the oracle (oracle/kdpt_oracle.c,
+  whose literal visited bitmap is where the reference itself writes nodeIDs[-1]): the differential
+  traversal test runs clean and still finds no mismatch.
+"""
+import json
+import os
+import subprocess
+
+import pytest
+
+from conftest import HAS_REFERENCE, ROOT, TESTS, REFERENCE
+from scene_text import write_scene_text
+from test_host_builder import EDGE_OBJS, MTL
+
+SAN = ["-fsanitize=address,undefined", "-fno-sanitize-recover=all", "-fno-omit-frame-pointer", "-g", "-O1"]
+ENV = dict(os.environ, ASAN_OPTIONS="detect_leaks=1:abort_on_error=0:halt_on_error=1",
+           UBSAN_OPTIONS="print_stacktrace=1:halt_on_error=1")
+CSRC = os.path.join(ROOT, "kdtreepathtraceroptimization_amd", "csrc")
+
+MALFORMED_OBJS = {
+    "missing_normals": "v 0 1 0\nv 1 1 0\nv 0 2 0\nf 1 2 3\n",
+    "short_normal_list": "v 0 1 0\nv 1 1 0\nv 0 2 0\nvn 0 0 1\nf 1//1 2//1 3//1\n",
+    "index_out_of_range": "v 0 1 0\nv 1 1 0\nv 0 2 0\nvn 0 0 1\nvn 0 0 1\nvn 0 0 1\nf 1 2 99\n",
+    "zero_index": "v 0 1 0\nv 1 1 0\nv 0 2 0\nvn 0 0 1\nvn 0 0 1\nvn 0 0 1\nf 0 1 2\n",
+    "negative_beyond_start": "v 0 1 0\nv 1 1 0\nv 0 2 0\nvn 0 0 1\nvn 0 0 1\nvn 0 0 1\nf -5 -6 -7\n",
+    "truncated_face": "v 0 1 0\nv 1 1 0\nvn 0 0 1\nvn 0 0 1\nf 1 2\n",
+    "garbage": "v a b c\nvn x y\nf x y z\n#\n\x01\x02\n",
+    "empty": "",
+    "inf_nan_coordinates": "v 1e38 1e39 -inf\nv nan 1 0\nv 0 2 0\nvn 0 0 1\nvn 0 0 1\nvn 0 0 1\nf 1 2 3\nf 3 2 1\n",
+    "long_line": "v " + "1" * 200000 + " 0 0\nv 1 1 0\nv 0 2 0\nvn 0 0 1\nvn 0 0 1\nvn 0 0 1\nf 1 2 3\n",
+    "missing_mtllib": "mtllib nowhere.mtl\nusemtl x\nv 0 1 0\nv 1 1 0\nv 0 2 0\nvn 0 0 1\nvn 0 0 1\n"
+                      "vn 0 0 1\nf 1 2 3\n",
+}
+MALFORMED_SCENES = {
+    "no_camera": "MATERIAL 0\nRGB 1 1 1\n\nOBJECT 0\ncube\nmaterial 0\nTRANS 0 0 0\nROTAT 0 0 0\nSCALE 1 1 1\n",
+    "truncated_material": "MATERIAL 0\nRGB 1\n",
+    "bad_indices": "MATERIAL 5\nRGB 1 1 1\n\nOBJECT 3\ncube\nmaterial 9\n",
+    "garbage": "\x00\x01 CAMERA\nRES -5 a\nFOVY\n",
+}
+
+
+@pytest.fixture(scope="module")
+def asan_host():
+    exe = os.path.join(ROOT, "build", "asan_host")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    subprocess.run(["g++", *SAN, "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-I", os.path.join(ROOT, "include"),
+                    os.path.join(TESTS, "native", "asan_host.cpp"), os.path.join(CSRC, "scene_host.cpp"),
+                    os.path.join(CSRC, "image_io.cpp"), "-o", exe], check=True)
+    return exe
+
+
+@pytest.fixture(scope="module")
+def files(tmp_path_factory):
+    d = tmp_path_factory.mktemp("san")
+    scene = write_scene_text("cornell", str(d / "scene.txt"), res=(32, 32))
+    (d / "t.mtl").write_text(MTL)
+    for k, v in {**EDGE_OBJS, **MALFORMED_OBJS}.items():
+        (d / f"{k}.obj").write_text(v)
+    for k, v in MALFORMED_SCENES.items():
+        (d / f"scene_{k}.txt").write_text(v)
+    return d, scene
+
+
+def _run(exe, scene, obj, nrays=300):
+    p = subprocess.run([exe, scene, obj, str(nrays)], capture_output=True, text=True, timeout=300, env=ENV)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert "runtime error" not in p.stderr and "Sanitizer" not in p.stderr, p.stderr[-4000:]
+    return json.loads(p.stdout.strip().splitlines()[-1])
+
+
+@pytest.mark.parametrize("name", sorted(EDGE_OBJS) + sorted(MALFORMED_OBJS))
+def test_host_builder_clean_under_sanitizers(asan_host, files, name):
+    d, scene = files
+    r = _run(asan_host, scene, str(d / f"{name}.obj"))
+    if name in EDGE_OBJS:
+        assert r["load_rc"] == 0 and r["nodes"] >= 1 and r["tris"] >= 1
+
+
+@pytest.mark.parametrize("name", sorted(MALFORMED_SCENES))
+def test_scene_parser_clean_under_sanitizers(asan_host, files, name):
+    d, _ = files
+    _run(asan_host, str(d / f"scene_{name}.txt"), "-")
+
+
+@pytest.mark.skipif(not HAS_REFERENCE, reason="/root/reference not present")
+@pytest.mark.parametrize("mesh", ["sphere_low_1", "dragon_5", "stanford_bunny"])
+def test_reference_meshes_clean_under_sanitizers(asan_host, mesh):
+    r = _run(asan_host, f"{REFERENCE}/scenes/cornell.txt", f"{REFERENCE}/scenes/{mesh}.obj", 2000)
+    assert r["load_rc"] == 0 and r["hits"] > 0
+
+
+@pytest.mark.skipif(not HAS_REFERENCE, reason="/root/reference not present")
+def test_oracle_and_traversal_clean_under_sanitizers():
+    exe = os.path.join(ROOT, "build", "traverse_diff_asan")
+    subprocess.run(["g++", *SAN, "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fopenmp", "-I",
+                    os.path.join(ROOT, "include"), "-x", "c++", os.path.join(TESTS, "native", "traverse_diff.cpp"),
+                    "-x", "c", os.path.join(ROOT, "oracle", "kdpt_oracle.c"), "-o", exe, "-lm"], check=True)
+    for mesh in ("sphere_low_1", "dragon_5"):
+        for hybrid in ("1", "0"):
+            p = subprocess.run([exe, f"{REFERENCE}/scenes/cornell.txt", f"{REFERENCE}/scenes/{mesh}.obj", "3000",
+                                "5", hybrid], capture_output=True, text=True, timeout=600, env=ENV)
+            assert p.returncode == 0, p.stderr[-4000:]
+            assert json.loads(p.stdout.strip().splitlines()[-1])["mismatches"] == 0
