@@ -536,6 +536,10 @@ template <int CTRL, int ROWS>
 __device__ inline unsigned long long dpp_u64(unsigned long long v) {
   return ((unsigned long long)dpp_u32<CTRL, ROWS>((uint32_t)(v >> 32)) << 32) | dpp_u32<CTRL, ROWS>((uint32_t)v);
 }
+__device__ inline unsigned long long readlane_u64(unsigned long long v, int lane) {
+  return ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), lane) << 32) |
+         (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, lane);
+}
 __device__ inline unsigned long long lane63_u64(unsigned long long v) {
   return ((unsigned long long)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), 63) << 32) |
          (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, 63);
@@ -807,22 +811,27 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       const int orig = fbits(T.e1.w);
       float bx = 0, by = 0, bzk = 0;
       const int r = tri_test_v(T, jo, jd, bx, by, bzk);
-      if (__ballot(r >= 1)) {
+      const unsigned long long m1 = __ballot(r >= 1);
+      if (m1) {
         const unsigned long long pk =
             r >= 1 ? ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk) : 0ull;
-        const unsigned long long wm = wave_max_u64(pk);
+        // usually one lane of the cluster passes: read its key instead of reducing over the wave
+        const unsigned long long wm = (m1 & (m1 - 1)) == 0ull ? readlane_u64(pk, __builtin_ctzll(m1))
+                                                              : wave_max_u64(pk);
         u_pass = wm > u_pass ? wm : u_pass;
         const unsigned long long m2 = __ballot(r == 2);
         if (m2) {
+          const bool one = (m2 & (m2 - 1)) == 0ull;
+          const int jh = __builtin_ctzll(m2);
           u_nhit += __builtin_popcountll(m2);
-          u_lasthit = max(u_lasthit, wave_max_i32(r == 2 ? orig : -1));
+          u_lasthit = max(u_lasthit, one ? __builtin_amdgcn_readlane(orig, jh) : wave_max_i32(r == 2 ? orig : -1));
           unsigned long long key = ~0ull;
           if (r == 2) {
             f3 hp, nn;
             const float t = tri_hit_t<HYBRID>(S, orig, jo, jd, bx, by, bzk, hp, nn);
             if (t > 0.0f) key = ((unsigned long long)f2u(t) << 32) | (unsigned int)orig;
           }
-          const unsigned long long wb = wave_min_u64(key);
+          const unsigned long long wb = one ? readlane_u64(key, jh) : wave_min_u64(key);
           u_best = wb < u_best ? wb : u_best;
         }
       }

@@ -1,7 +1,7 @@
 #!/bin/bash
 # One GPU-box session (run from the repo root through gpurun):
 #   bash tools/gpu_session.sh TAG "STEP;STEP;..."
-# Steps: tests | smoke | bench:<args> | gloo2:<args> (two ranks sharing the GPU, gloo reduce) | py:<args> | sh:<cmd>
+# Steps: tests[:pytest args, shell-quoted] | smoke | bench:<args> | gloo2:<args> (two ranks sharing the GPU, gloo reduce) | py:<args> | sh:<cmd>
 # Every step has its own time limit; a fault, abort, segfault or time-out ends the session there
 # (pytest assertion failures, exit 1, do not).  Logs go to gpurun_out/<TAG>/.
 TAG=${1:?tag}
@@ -19,7 +19,7 @@ for step in "${LIST[@]}"; do
   log="$OUT/$(printf %02d $n)_${kind}.log"
   echo "[session] step $n: $kind $args -> $log"
   case "$kind" in
-    tests) timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread --maxfail 30 $args > "$log" 2>&1 ;;
+    tests) eval "timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 300 --timeout-method thread --maxfail 30 $args" > "$log" 2>&1 ;;
     smoke) timeout -k 10 300 python -u -c "import __graft_entry__ as g; g.smoke()" > "$log" 2>&1 ;;
     bench) timeout -k 10 600 python -u bench.py $args > "$log" 2>&1 ;;
     gloo2) timeout -k 10 600 python -u -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
