@@ -244,8 +244,11 @@ int kdpt_count_split(kdpt_ctx *ctx, unsigned long long *aabb_prep_cand);
 /* Diagnostic: cycle profile of the intersect kernel during the last kdpt_count_iteration.
  * Copies up to n values -- node trips, node cycles, big-leaf sweeps, big-leaf cycles,
  * small-leaf phases, small-leaf rounds, small-leaf cycles, recombination cycles, setup
- * cycles, analytic-geometry cycles, post cycles, spare (each summed over 64-path chunks),
- * chunks, chunk cycles, aabb, tri, hit, then a 64-bin histogram of intersect-wave lifetimes
+ * cycles, analytic-geometry cycles, post cycles, node lane-steps, big leaves swept, their
+ * clusters, clusters tested with a u/v pass, ... with several, small-leaf (ray, triangle) pairs,
+ * node-trip lanes waiting on a leaf, ... finished, cycles after the ray queue ran dry, finished
+ * node-trip lanes then (each summed over waves), waves, wave cycles, aabb, tri, hit, then a 64-bin
+ * histogram of intersect-wave lifetimes
  * (10 us bins) -- and returns how many exist. */
 int kdpt_wave_profile(kdpt_ctx *ctx, unsigned long long *out, int n);
 /* Device-math known answers: sinf/cosf/pow-5 Fresnel/u01 evaluated by the gfx950 code. */

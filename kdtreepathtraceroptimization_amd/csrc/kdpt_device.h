@@ -477,7 +477,9 @@ struct NodesPacked {
 // wave-profile slots (count mode): trips / cycles of each part of the intersect kernel
 enum ProfSlot {
   PROF_NODE_TRIPS, PROF_NODE_CYC, PROF_BIG_SWEEPS, PROF_BIG_CYC, PROF_SMALL_PHASES, PROF_SMALL_ROUNDS,
-  PROF_SMALL_CYC, PROF_FINAL_CYC, PROF_SETUP_CYC, PROF_GEOM_CYC, PROF_POST_CYC, PROF_SPARE, PROF_SLOTS
+  PROF_SMALL_CYC, PROF_FINAL_CYC, PROF_SETUP_CYC, PROF_GEOM_CYC, PROF_POST_CYC, PROF_SPARE,
+  PROF_BIG_LEAVES, PROF_BIG_CLUSTERS, PROF_BIG_PASS, PROF_BIG_MULTI, PROF_SMALL_PAIRS, PROF_NODE_LEAFWAIT,
+  PROF_NODE_DONE, PROF_TAIL_CYC, PROF_TAIL_NODE_DONE, PROF_SLOTS
 };
 
 // Cluster boxes of the big leaves: separate lo/hi arrays (HBM) or interleaved lo, hi (LDS copy).
@@ -503,7 +505,8 @@ struct WaveLeafLDS {
   int nhit[64];
   unsigned long long best[64];  // (t bits << 32) | triangle index, min
   // count mode only, kept by lane 0 (slots: PROF_* below); last timestamp
-  unsigned long long prof[12];
+  unsigned long long prof[PROF_SLOTS];
+  unsigned long long tail_t0;  // count mode: the wave's clock when its ray queue ran dry
   unsigned long long tlast;
 };
 
@@ -691,6 +694,10 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     if (COUNT) {
       trips += walk ? 1 : 0;
       prof_add(W, PROF_SPARE, (unsigned long long)__popcll(wmask));  // lane-steps: SIMD efficiency
+      prof_add(W, PROF_NODE_LEAFWAIT, (unsigned long long)__popcll(__ballot((fl & F_LEAF) != 0u)));
+      const unsigned long long nd_done = (unsigned long long)__popcll(__ballot((fl & F_DONE) != 0u));
+      prof_add(W, PROF_NODE_DONE, nd_done);
+      if (W->tail_t0) prof_add(W, PROF_TAIL_NODE_DONE, nd_done);
     }
     const NodeRec nd = nodes(cur < 0 ? 0 : cur);
     const int left = nd.left, right = nd.right;
@@ -779,6 +786,10 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     const f3 jd = mk3(readlane_f(d.x, j), readlane_f(d.y, j), readlane_f(d.z, j));
     const f3 jinv = mk3(readlane_f(invdir.x, j), readlane_f(invdir.y, j), readlane_f(invdir.z, j));
     const int2 cr = make_int2(jfirst, jcount);
+    if (COUNT) {
+      prof_add(W, PROF_BIG_LEAVES, 1);
+      prof_add(W, PROF_BIG_CLUSTERS, (unsigned long long)jcount);
+    }
     unsigned long long u_pass = 0ull, u_best = ~0ull;
     int u_lasthit = -1, u_nhit = 0;
     for (int cb0 = 0; cb0 < cr.y; cb0 += 64) {
@@ -812,6 +823,10 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       float bx = 0, by = 0, bzk = 0;
       const int r = tri_test_v(T, jo, jd, bx, by, bzk);
       const unsigned long long m1 = __ballot(r >= 1);
+      if (COUNT && m1) {
+        prof_add(W, PROF_BIG_PASS, 1);
+        prof_add(W, PROF_BIG_MULTI, (m1 & (m1 - 1)) ? 1 : 0);
+      }
       if (m1) {
         const unsigned long long pk =
             r >= 1 ? ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk) : 0ull;
@@ -866,7 +881,10 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     W->nhit[lane] = 0;
     W->best[lane] = ~0ull;
     wave_lds_sync();
-    if (COUNT) prof_add(W, PROF_SMALL_ROUNDS, (unsigned long long)((P + 63) / 64));
+    if (COUNT) {
+      prof_add(W, PROF_SMALL_ROUNDS, (unsigned long long)((P + 63) / 64));
+      prof_add(W, PROF_SMALL_PAIRS, (unsigned long long)P);
+    }
     // pair pi -> owner lane (binary search over the inclusive ends) and triangle; the next
     // round's pair is located and its triangle loaded while the current one is tested
     auto owner_of = [&](int q) {

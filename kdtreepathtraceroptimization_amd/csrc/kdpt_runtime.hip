@@ -156,7 +156,10 @@ __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int
 // same functions, so nothing else needs to travel.
 // ---------------------------------------------------------------------------
 enum TreeMode { TREE_WIDE = 0, TREE_PACKED = 1, TREE_LDS = 2 };
-constexpr int TRACE_BLOCK = 1024;  // LDS mode: one workgroup per CU shares the tree copy
+#ifndef KDPT_TRACE_BLOCK
+#define KDPT_TRACE_BLOCK 1024  // tools/build_variant.sh experiments only
+#endif
+constexpr int TRACE_BLOCK = KDPT_TRACE_BLOCK;  // LDS mode: one workgroup per CU shares the tree copy
 #ifndef KDPT_SRUN_SPREAD
 #define KDPT_SRUN_SPREAD 0  // 1: static runs of ceil(n / waves) instead of 64 (experiment)
 #endif
@@ -363,6 +366,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
   const int lane = threadIdx.x & 63;
   WaveLeafLDS* W = &s_leaf[threadIdx.x >> 6];
   if (COUNT && lane < PROF_SLOTS) W->prof[lane] = 0;
+  if (COUNT && lane == 0) W->tail_t0 = 0;
   // launch duration on the device clock (first block start .. last block end); the HIP events around
   // the launch also count time spent queued behind other streams' kernels when iterations overlap
   __shared__ int s_waves_done;
@@ -412,6 +416,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
         k = base + p;
         exhausted = base + __popcll(im) >= n;  // the counter only grows: later rounds find nothing
       }
+      if (COUNT && exhausted && lane == 0 && !W->tail_t0) W->tail_t0 = __builtin_readcyclecounter();
       if (pidx < 0 && k < n) {
         const int b = (k >= pre[1]) + (k >= pre[2]) + (k >= pre[3]);
         const TraceIter& I = b == 0 ? A.it[0] : (b == 1 ? A.it[1] : (b == 2 ? A.it[2] : A.it[3]));
@@ -456,6 +461,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
   }
   if (COUNT) {
     prof_lap(W, PROF_POST_CYC);
+    if (lane == 0 && W->tail_t0) W->prof[PROF_TAIL_CYC] += __builtin_readcyclecounter() - W->tail_t0;
     flush_counters(A.counters, cnt, W, t_k0);
     if (lane == 0) {
       const unsigned long long us10 = (__builtin_amdgcn_s_memrealtime() - rt0) / 1000;  // 100 MHz ticks
@@ -2199,7 +2205,8 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
   // concurrent launches on disjoint CU subsets overlap those tails instead of queueing behind them.
   for (auto sl : c->slots)
     sl->trace_grid = c->grid_env ? c->trace_grid : std::max(1, c->trace_grid * 2 / std::max(2, depth));
-  c->stats.intersect_grid_share = c->slots.empty() ? 1.0f : (float)c->slots[0]->trace_grid / (float)c->trace_grid;
+  c->stats.intersect_grid_share =
+      c->slots.empty() ? 1.0f : (float)c->slots[0]->trace_grid / (float)std::max(1, c->full_trace_grid);
   // diagnostic ("profile_batches" knob): the counting intersect kernel (kdpt_wave_profile after sync)
   if (c->profile_batches) HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(Counters), c->stream));
   for (int kb = 0, bi = 0; kb < count; kb += B, bi++) {

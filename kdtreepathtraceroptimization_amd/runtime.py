@@ -451,6 +451,8 @@ class PathTracer:
         _check(0 if n > 0 else n, "kdpt_wave_profile")
         keys = ("node_trips", "node_cycles", "big_sweeps", "big_cycles", "small_phases", "small_rounds",
                 "small_cycles", "final_cycles", "setup_cycles", "geom_cycles", "post_cycles", "node_lane_steps",
+                "big_leaves", "big_clusters", "big_pass", "big_multi", "small_pairs", "node_leafwait_steps",
+                "node_done_steps", "tail_cycles", "tail_node_done_steps",
                 "chunks", "chunk_cycles", "aabb", "tri", "hit")
         prof = dict(zip(keys, (int(out[k]) for k in range(len(keys)))))
         if n > len(keys):

@@ -19,6 +19,9 @@ for cfg in (sys.argv[2] if len(sys.argv) > 2 else "1x1,2x2,1x4").split(","):
     pt.synchronize()
     prof = pt.wave_profile()
     prof.pop("wave_life_10us", None)
+    rays = max(1, pt.stats().total_trace_rays)
+    print(json.dumps({"cfg": cfg, "rays": rays, "per_ray": {k: round(v / rays, 3) for k, v in prof.items()}}),
+          flush=True)
     w = max(1, prof["chunks"])
     eff = prof["node_lane_steps"] / max(1, prof["node_trips"]) / 64
     print(json.dumps({"cfg": cfg, "waves": w, "node_trips_per_wave": round(prof["node_trips"] / w, 1),

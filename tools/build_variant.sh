@@ -1,0 +1,13 @@
+#!/bin/bash
+# Build an A/B variant of libkdpt.so into ab/NAME.so with extra compile flags (e.g. -DKDPT_TRACE_BLOCK=512);
+# the host objects come from the regular in-tree build (run _build first).
+#   bash tools/build_variant.sh NAME [hipcc flags...]
+set -e
+NAME=$1; shift
+ROOT=$(cd "$(dirname "$0")/.." && pwd)
+mkdir -p "$ROOT/ab" "$ROOT/build/ab"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I "$ROOT/include" "$@" \
+  -c "$ROOT/kdtreepathtraceroptimization_amd/csrc/kdpt_runtime.hip" -o "$ROOT/build/ab/$NAME.o"
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/ab/$NAME.so" "$ROOT/build/ab/$NAME.o" \
+  "$ROOT/build/scene_host.o" "$ROOT/build/image_io.o"
+echo "ab/$NAME.so"
