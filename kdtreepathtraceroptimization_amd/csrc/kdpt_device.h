@@ -599,14 +599,19 @@ __device__ inline int tri_test(const DevScene& S, int i, f3 o, f3 d, float& bx, 
 
 
 template <bool HYBRID>
-__device__ inline float tri_hit_t(const DevScene& S, int i, f3 o, f3 d, float bx, float by, float bz, f3& hit,
-                                  f3& norm) {
-  const float4 n1v = S.tn0[i], n2v = S.tn1[i], n3v = S.tn2[i];
+__device__ inline float tri_hit_t_n(float4 n1v, float4 n2v, float4 n3v, f3 o, f3 d, float bx, float by, float bz,
+                                    f3& hit, f3& norm) {
   const float w0 = 1 - bx - by;
   norm = normalize(add(add(scl(mk3(n1v.x, n1v.y, n1v.z), w0), scl(mk3(n2v.x, n2v.y, n2v.z), bx)),
                        scl(mk3(n3v.x, n3v.y, n3v.z), by)));
   hit = add(add(o, scl(d, bz)), scl(norm, HYBRID ? 0.0001f : 0.00001f));
   return distance(o, hit);
+}
+
+template <bool HYBRID>
+__device__ inline float tri_hit_t(const DevScene& S, int i, f3 o, f3 d, float bx, float by, float bz, f3& hit,
+                                  f3& norm) {
+  return tri_hit_t_n<HYBRID>(S.tn0[i], S.tn1[i], S.tn2[i], o, d, bx, by, bz, hit, norm);
 }
 
 // One lane's ray and traversal state: exactly traverseKD's locals, kept across trace_phase calls so

@@ -764,6 +764,13 @@ __device__ __attribute__((always_inline)) inline void shade_one(const ShadeArgs&
   f3 color = mk3(q2.x, q2.y, q2.z);
   int bounces = fbits(q2.w);
   o.changed = bounces > 0;
+  // the pixel's accumulated value (partialGather below), fetched with the hit's triangle instead of after
+  // the shading: one dependent HBM round trip less for the paths that end at this bounce
+  float3 px_old = make_float3(0.0f, 0.0f, 0.0f);
+  if (COMPACT) {
+    const float* px = A.image + 3 * (size_t)pix;
+    px_old = make_float3(px[0], px[1], px[2]);
+  }
   if (bounces > 0) {
     float isect_t = -1.0f;
     int isect_mat = 0;
@@ -773,9 +780,12 @@ __device__ __attribute__((always_inline)) inline void shade_one(const ShadeArgs&
       int mid;
       if (hr.x < -1) {  // triangle: the traversal's final recomputation, repeated
         const int k = -hr.x - 2;
+        // all six records in flight at once (vertex, edges, normals), then the arithmetic
+        const TriData T{S.tv0[k], S.te1[k], S.te2[k]};
+        const float4 n1v = S.tn0[k], n2v = S.tn1[k], n3v = S.tn2[k];
         float bx, by, bzk;
-        tri_test(S, k, ray.origin, ray.direction, bx, by, bzk);
-        t = tri_hit_t<HYBRID>(S, k, ray.origin, ray.direction, bx, by, bzk, ip, nrm);
+        tri_test_v(T, ray.origin, ray.direction, bx, by, bzk);
+        t = tri_hit_t_n<HYBRID>(n1v, n2v, n3v, ray.origin, ray.direction, bx, by, bzk, ip, nrm);
         mid = hr.y;
       } else {
         const DevGeom& G = S.geoms[hr.x];
@@ -797,9 +807,9 @@ __device__ __attribute__((always_inline)) inline void shade_one(const ShadeArgs&
   if (COMPACT && bounces == 0) {
     // partialGather: one live path per pixel, so this read-modify-write never collides
     float* px = A.image + 3 * (size_t)pix;
-    px[0] += color.x;
-    px[1] += color.y;
-    px[2] += color.z;
+    px[0] = px_old.x + color.x;
+    px[1] = px_old.y + color.y;
+    px[2] = px_old.z + color.z;
   }
   o.alive = COMPACT ? (bounces != 0) : true;
   o.walk = o.tested = false;
