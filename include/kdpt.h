@@ -218,6 +218,12 @@ int kdpt_hdr_encode(const float *rgb, int w, int h, uint8_t **out, size_t *len);
 int kdpt_write_hdr(const char *path, const float *rgb, int w, int h);
 void kdpt_free(void *p);
 int kdpt_get_stats(kdpt_ctx *ctx, kdpt_stats *st);
+/* pathtrace()'s per-call flags without a new context: focal_length, dof_angle, softness, cacherays,
+ * antialias, enable_sss, testing_mode, compaction and short_stack take effect from the next iteration
+ * (the accumulation image is kept).  enable_kd, viz_kd, use_bbox, bounce_cap, block_size and
+ * external_image must equal the context's (KDPT_ERR_UNSUPPORTED otherwise: they decide what
+ * kdpt_create uploads and allocates). */
+int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
 /* Explicit A/B and diagnostic knobs (the library reads no environment variables; a context created
  * without this call always runs the tested default route).  Names: "shade_fused" (1; 0 = k_shade +
  * k_scan + k_scatter), "early_walk" (32) / "early_leaf" (24) (node-phase hand-over thresholds),

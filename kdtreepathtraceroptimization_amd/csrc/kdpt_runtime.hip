@@ -2053,6 +2053,37 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   return KDPT_OK;
 }
 
+int kdpt_set_options(kdpt_ctx* c, const kdpt_options* o) {
+  if (!c || !o) return fail(KDPT_ERR_ARG, "null arg");
+  if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
+  const kdpt_options& p = c->opt;
+  // these select what is uploaded or how much is allocated: a new context is needed
+  if (o->enable_kd != p.enable_kd || o->viz_kd != p.viz_kd || o->use_bbox != p.use_bbox ||
+      (o->bounce_cap > 0 ? o->bounce_cap : 8) != c->cap || o->block_size != p.block_size ||
+      o->external_image != p.external_image)
+    return fail(KDPT_ERR_UNSUPPORTED, "enable_kd, viz_kd, use_bbox, bounce_cap, block_size and external_image "
+                                      "are fixed at kdpt_create");
+  HIP_TRY(hipSetDevice(c->device));
+  if (!c->slots.empty()) {  // iterations in flight keep the options they were enqueued with
+    int rc = kdpt_synchronize(c);
+    if (rc) return rc;
+  }
+  auto apply = [o](kdpt_options& d) {
+    d.focal_length = o->focal_length;
+    d.dof_angle = o->dof_angle;
+    d.softness = o->softness;
+    d.cacherays = o->cacherays;
+    d.antialias = o->antialias;
+    d.enable_sss = o->enable_sss;
+    d.testing_mode = o->testing_mode;
+    d.compaction = o->compaction;
+    d.short_stack = o->short_stack;
+  };
+  apply(c->opt);
+  for (auto sl : c->slots) apply(sl->opt);
+  return KDPT_OK;
+}
+
 int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
   if (!c || !name) return fail(KDPT_ERR_ARG, "null arg");
   if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");

@@ -112,7 +112,7 @@ EXPORTS = [
     "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_count_split", "kdpt_wave_profile", "kdpt_selftest_math", "kdpt_selftest_rng",
     "kdpt_selftest_fresnel", "kdpt_selftest_libm", "kdpt_selftest_libm_digest", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
     "kdpt_save_rgb8", "kdpt_save_png", "kdpt_save_hdr", "kdpt_png_encode", "kdpt_write_png", "kdpt_hdr_encode",
-    "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm",
+    "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm", "kdpt_set_options",
 ]
 
 _lib = None
@@ -170,6 +170,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_write_hdr.argtypes = [C.c_char_p, P(C.c_float), C.c_int, C.c_int]
     lib.kdpt_free.argtypes = [C.c_void_p]
     lib.kdpt_free.restype = None
+    if hasattr(lib, "kdpt_set_options"):
+        lib.kdpt_set_options.argtypes = [C.c_void_p, P(Options)]
     if hasattr(lib, "kdpt_selftest_glm"):
         lib.kdpt_selftest_glm.argtypes = [C.c_int, P(C.c_float), C.c_int, P(C.c_float)]
     if hasattr(lib, "kdpt_set_tuning"):  # absent from older builds used in A/B runs
@@ -389,6 +391,11 @@ class PathTracer:
         _check(self.lib.kdpt_write_pbo(self._ctx, int(iteration), out.ctypes.data_as(C.POINTER(C.c_uint8))),
                "kdpt_write_pbo")
         return out
+
+    def set_options(self, options: Options):
+        """kdpt_set_options: pathtrace()'s per-call flags for the next iterations (same context)."""
+        _check(self.lib.kdpt_set_options(self._ctx, C.byref(options)), "kdpt_set_options")
+        self.opt = options
 
     def set_tuning(self, name: str, value: float):
         """kdpt_set_tuning: an explicit A/B or diagnostic knob (the library reads no environment)."""

@@ -1,0 +1,77 @@
+"""The drop-in shim (integration/pathtrace_kdpt.cpp): the reference's pathtraceInit /
+pathtrace / pathtraceFree (src/pathtrace.h:6-21) over include/kdpt.h.
+
+CPU: the shim and a driver that calls it the way src/main.cpp does compile against include/kdpt.h and a
+layout-identical stand-in of the reference's Scene (tests/native/shim/pathtrace.h) and link against
+libkdpt.so -- any drift between the shim and the C-ABI fails here.  GPU: the driver renders through the
+shim (per-call flags applied with kdpt_set_options, no re-upload) and the image equals the oracle's
+render of the same scene files bit for bit."""
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+from conftest import ROOT, TESTS
+from kdtreepathtraceroptimization_amd.meshes import write_obj
+from scene_text import write_scene_text
+
+LIBDIR = os.path.join(ROOT, "kdtreepathtraceroptimization_amd")
+
+
+@pytest.fixture(scope="module")
+def shim_driver(kdpt):
+    exe = os.path.join(ROOT, "build", "shim_driver")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-Wall", "-Werror", "-I", os.path.join(ROOT, "include"), "-I",
+                    os.path.join(TESTS, "native", "shim"), os.path.join(ROOT, "integration", "pathtrace_kdpt.cpp"),
+                    os.path.join(TESTS, "native", "shim_driver.cpp"), "-L", LIBDIR, "-lkdpt",
+                    "-Wl,-rpath," + LIBDIR, "-o", exe], check=True)
+    return exe
+
+
+def test_shim_compiles_and_links_against_the_c_abi(shim_driver):
+    assert os.path.exists(shim_driver)
+
+
+def test_scene_stand_in_matches_reference_layouts(kdpt):
+    """The stand-in's structs are the reference's layouts, as include/kdpt.h's are."""
+    src = r'''
+#include <cstddef>
+#include <cstdio>
+#include "pathtrace.h"
+#include "kdpt.h"
+int main() {
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(Geom), sizeof(Material), sizeof(Camera), sizeof(KDN::NodeBare),
+         sizeof(KDN::TriBare), offsetof(Geom, invTranspose), offsetof(Material, transmittance));
+  printf("%zu %zu %zu %zu %zu %zu %zu\n", sizeof(kdpt_geom), sizeof(kdpt_material), sizeof(kdpt_camera),
+         sizeof(kdpt_node_bare), sizeof(kdpt_tri_bare), offsetof(kdpt_geom, invTranspose),
+         offsetof(kdpt_material, transmittance));
+}'''
+    exe = os.path.join(ROOT, "build", "shim_layout")
+    cpp = exe + ".cpp"
+    open(cpp, "w").write(src)
+    subprocess.run(["g++", "-std=c++17", "-I", os.path.join(ROOT, "include"), "-I", os.path.join(TESTS, "native", "shim"),
+                    cpp, "-o", exe], check=True)
+    a, b = subprocess.run([exe], capture_output=True, text=True, check=True).stdout.split("\n")[:2]
+    assert a == b
+    assert a.split()[:5] == ["236", "56", "84", "64", "76"]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("flags", [("0", "0", "0", "1", "1", "1"), ("0.5", "0.03", "1", "1", "1", "1"),
+                                   ("0", "0", "0", "0", "0", "1"), ("0", "0", "0", "1", "1", "0")])
+def test_shim_render_equals_oracle(shim_driver, oracle, tmp_path, flags):
+    scene = write_scene_text("cornell", str(tmp_path / "cornell.txt"))
+    obj = str(tmp_path / "ico.obj")
+    write_obj(obj, 3)
+    out = str(tmp_path / "img.f32")
+    subprocess.run([shim_driver, scene, obj, "40", "32", "3", out, *flags], check=True, timeout=120)
+    img = np.fromfile(out, np.float32).reshape(32, 40, 3)
+    softness, dof, sss, shortstack, compaction, enablekd = flags
+    s = oracle.OracleScene.from_files(scene, obj, res=(40, 32))
+    ref, _ = s.render(1, 3, softness=float(np.float32(softness)), dofAngle=float(np.float32(dof)),
+                      enableSss=int(sss), shortstack=int(shortstack), compaction=int(compaction),
+                      enable_kd=int(enablekd))
+    assert np.array_equal(img.view(np.uint32), ref.view(np.uint32))
