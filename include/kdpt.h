@@ -304,6 +304,17 @@ typedef struct kdpt_scene_desc {
     int kd_max_depth;               /* 0 = 13, the reference's split(13) */
 } kdpt_scene_desc;
 int kdpt_scene_build(const kdpt_scene_desc *desc, kdpt_scene_data **out);
+/* The same, with the KD tree built on GPU `device` (csrc/kd_build.hip: level by level, breadth first, then
+ * pre-order IDs) instead of the host recursion; the arrays are byte-identical to kdpt_scene_build's
+ * (KDnode::split src/KDnode.cpp:151-249, Scene::loadObj src/scene.cpp:866-968). */
+int kdpt_scene_build_device(const kdpt_scene_desc *desc, int device, kdpt_scene_data **out);
+/* Wall time of the GPU KD build of a kdpt_scene_build_device scene (0 for a host build). */
+int kdpt_scene_kd_build_ms(const kdpt_scene_data *sd, double *ms);
+/* The GPU KD build alone over a triangle soup (9 vertex + 9 normal floats and an mtlIdx per triangle, the
+ * reference's Triangle order): NodeBare[] in ID order and TriBare[] in leaf order, malloc'd (kdpt_free). */
+int kdpt_build_kd_device(const float *verts9, const float *norms9, const int *mtl, int ntri, int maxdepth,
+                         int device, kdpt_node_bare **nodes, int *nnodes, kdpt_tri_bare **tris, int *ntris,
+                         double *ms);
 /* View of the built scene as the C-ABI struct (pointers owned by the scene data). */
 int kdpt_scene_view(const kdpt_scene_data *sd, kdpt_scene *out);
 int kdpt_scene_free(kdpt_scene_data *sd);

@@ -56,7 +56,9 @@ def build(force: bool = False) -> str:
     host_obj = os.path.join(BUILD, "scene_host.o")
     io_obj = os.path.join(BUILD, "image_io.o")
     dev_obj = os.path.join(BUILD, "kdpt_runtime.o")
+    kd_obj = os.path.join(BUILD, "kd_build.o")
     _run(["g++", *COMMON, "-c", os.path.join(CSRC, "scene_host.cpp"), "-o", host_obj])
+    _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-c", os.path.join(CSRC, "kd_build.hip"), "-o", kd_obj])
     _run(["g++", *COMMON, "-c", os.path.join(CSRC, "image_io.cpp"), "-o", io_obj])
     # the per-kernel resource report (VGPRs, scratch, occupancy) goes to the build log, which
     # tests/test_build_resources.py checks: a hot kernel that starts spilling or calling out-of-line
@@ -64,7 +66,7 @@ def build(force: bool = False) -> str:
     _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-Rpass-analysis=kernel-resource-usage", "-c",
           os.path.join(CSRC, "kdpt_runtime.hip"), "-o", dev_obj], log=RESOURCE_LOG)
     tmp = LIB + ".tmp"
-    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, dev_obj, host_obj, io_obj])
+    _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, dev_obj, kd_obj, host_obj, io_obj])
     os.replace(tmp, LIB)
     return LIB
 

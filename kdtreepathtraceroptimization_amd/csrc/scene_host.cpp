@@ -25,6 +25,8 @@
 #include <map>
 #include <memory>
 #include <sstream>
+
+#include "kd_build.h"
 #include <string>
 #include <vector>
 
@@ -46,6 +48,7 @@ struct kdpt_scene_data {
   // the raw OBJ arrays of the brute-force mode (src/scene.cpp:603-712), in triangle-soup form
   std::vector<float> obj_verts, obj_norms, obj_bboxes;
   std::vector<int> obj_polyoffsets, obj_polysidxflat;
+  double kd_build_ms = 0.0;  // kdpt_scene_build_device: the GPU KD build's wall time
 };
 
 namespace {
@@ -315,8 +318,8 @@ void preorder(Node* n, std::vector<Node*>& out) {
 // Scene::loadObj KD section (src/scene.cpp:866-968): IDs are assigned in pre-order,
 // so the ID-sorted node list is the pre-order walk; leaves' triangles are listed in
 // that order (duplicates included).
-void build_kd(const float* v9, const float* n9, const int* mtl, int ntri, int maxdepth,
-              std::vector<kdpt_node_bare>& nodes_out, std::vector<kdpt_tri_bare>& tris_out) {
+void build_kd_impl(const float* v9, const float* n9, const int* mtl, int ntri, int maxdepth,
+                   std::vector<kdpt_node_bare>& nodes_out, std::vector<kdpt_tri_bare>& tris_out) {
   std::vector<Tri> T(ntri);
   for (int i = 0; i < ntri; i++) {
     const float* v = v9 + 9 * (size_t)i;
@@ -871,6 +874,11 @@ void obj_arrays(const kdpt_scene_desc& d, kdpt_scene_data& sd) {
 }  // namespace
 
 namespace kdpt_host {
+void build_kd(const float* v9, const float* n9, const int* mtl, int ntri, int maxdepth,
+              std::vector<kdpt_node_bare>& nodes_out, std::vector<kdpt_tri_bare>& tris_out) {
+  build_kd_impl(v9, n9, mtl, ntri, maxdepth, nodes_out, tris_out);
+}
+
 // boxIntersectionTestBox's matrices for a KD node (src/intersections.h:51-63): the unit cube scaled by
 // maxs - mins, moved to (mins + maxs) * 0.5 (double product -> float, glm::mat4's converting
 // constructor), and its glm::inverse (the same restatement the analytic geoms use).
@@ -888,7 +896,9 @@ void node_box_matrices(const float* mins, const float* maxs, float* transform16,
 
 extern "C" {
 
-int kdpt_scene_build(const kdpt_scene_desc* d, kdpt_scene_data** out) {
+namespace {
+// Scene::Scene + Scene::loadObj from parsed values; the KD tree on the host (device < 0) or on the GPU
+int scene_build(const kdpt_scene_desc* d, int device, kdpt_scene_data** out) {
   if (!d || !out) return KDPT_ERR_ARG;
   *out = nullptr;
   if (d->res[0] <= 0 || d->res[1] <= 0) return KDPT_ERR_ARG;
@@ -918,14 +928,56 @@ int kdpt_scene_build(const kdpt_scene_desc* d, kdpt_scene_data** out) {
       sd->obj_materialOffsets.push_back((int)sd->materials.size());
       sd->materials.push_back(d->shape_materials[i]);
     }
-    build_kd(d->verts9, d->norms9, d->shape_of_tri, d->ntri, d->kd_max_depth > 0 ? d->kd_max_depth : 13,
-             sd->nodes, sd->tris);
+    const int maxdepth = d->kd_max_depth > 0 ? d->kd_max_depth : 13;
+    if (device < 0) {
+      kdpt_host::build_kd(d->verts9, d->norms9, d->shape_of_tri, d->ntri, maxdepth, sd->nodes, sd->tris);
+    } else {
+      const int rc = kdpt_host::build_kd_device(d->verts9, d->norms9, d->shape_of_tri, d->ntri, maxdepth, device,
+                                                sd->nodes, sd->tris, &sd->kd_build_ms);
+      if (rc) return rc;
+    }
     sd->has_obj = true;
     obj_arrays(*d, *sd);
   }
   *out = sd.release();
   return KDPT_OK;
 }
+}  // namespace
+
+int kdpt_scene_build(const kdpt_scene_desc* d, kdpt_scene_data** out) { return scene_build(d, -1, out); }
+
+int kdpt_scene_build_device(const kdpt_scene_desc* d, int device, kdpt_scene_data** out) {
+  if (device < 0) return KDPT_ERR_ARG;
+  return scene_build(d, device, out);
+}
+
+int kdpt_scene_kd_build_ms(const kdpt_scene_data* sd, double* ms) {
+  if (!sd || !ms) return KDPT_ERR_ARG;
+  *ms = sd->kd_build_ms;
+  return KDPT_OK;
+}
+
+int kdpt_build_kd_device(const float* verts9, const float* norms9, const int* mtl, int ntri, int maxdepth, int device,
+                         kdpt_node_bare** nodes, int* nnodes, kdpt_tri_bare** tris, int* ntris, double* ms) {
+  if (!verts9 || !norms9 || !mtl || ntri < 0 || !nodes || !nnodes || !tris || !ntris) return KDPT_ERR_ARG;
+  std::vector<kdpt_node_bare> nv;
+  std::vector<kdpt_tri_bare> tv;
+  const int rc = kdpt_host::build_kd_device(verts9, norms9, mtl, ntri, maxdepth > 0 ? maxdepth : 13, device, nv, tv, ms);
+  if (rc) return rc;
+  *nodes = (kdpt_node_bare*)malloc(std::max<size_t>(1, nv.size()) * sizeof(kdpt_node_bare));
+  *tris = (kdpt_tri_bare*)malloc(std::max<size_t>(1, tv.size()) * sizeof(kdpt_tri_bare));
+  if (!*nodes || !*tris) {
+    free(*nodes);
+    free(*tris);
+    return KDPT_ERR_ARG;
+  }
+  if (!nv.empty()) memcpy(*nodes, nv.data(), nv.size() * sizeof(kdpt_node_bare));
+  if (!tv.empty()) memcpy(*tris, tv.data(), tv.size() * sizeof(kdpt_tri_bare));
+  *nnodes = (int)nv.size();
+  *ntris = (int)tv.size();
+  return KDPT_OK;
+}
+
 
 int kdpt_scene_load(const char* scene_path, const char* obj_path, int res_w, int res_h, int depth,
                     kdpt_scene_data** out) {

@@ -112,7 +112,8 @@ EXPORTS = [
     "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_count_split", "kdpt_wave_profile", "kdpt_selftest_math", "kdpt_selftest_rng",
     "kdpt_selftest_fresnel", "kdpt_selftest_libm", "kdpt_selftest_libm_digest", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
     "kdpt_save_rgb8", "kdpt_save_png", "kdpt_save_hdr", "kdpt_png_encode", "kdpt_write_png", "kdpt_hdr_encode",
-    "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm", "kdpt_set_options",
+    "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm", "kdpt_set_options", "kdpt_scene_build_device",
+    "kdpt_scene_kd_build_ms", "kdpt_build_kd_device",
 ]
 
 _lib = None
@@ -170,6 +171,11 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_write_hdr.argtypes = [C.c_char_p, P(C.c_float), C.c_int, C.c_int]
     lib.kdpt_free.argtypes = [C.c_void_p]
     lib.kdpt_free.restype = None
+    if hasattr(lib, "kdpt_scene_build_device"):
+        lib.kdpt_scene_build_device.argtypes = [P(SceneDesc), C.c_int, P(C.c_void_p)]
+        lib.kdpt_scene_kd_build_ms.argtypes = [C.c_void_p, P(C.c_double)]
+        lib.kdpt_build_kd_device.argtypes = [P(C.c_float), P(C.c_float), P(C.c_int), C.c_int, C.c_int, C.c_int,
+                                             P(C.c_void_p), P(C.c_int), P(C.c_void_p), P(C.c_int), P(C.c_double)]
     if hasattr(lib, "kdpt_set_options"):
         lib.kdpt_set_options.argtypes = [C.c_void_p, P(Options)]
     if hasattr(lib, "kdpt_selftest_glm"):
@@ -218,6 +224,7 @@ class SceneDescription:
     norms9: Optional[np.ndarray] = None   # float32[ntri, 9]
     shape_of_tri: Optional[np.ndarray] = None  # int32[ntri]
     shape_materials: Optional[np.ndarray] = None  # MATERIAL_DTYPE[nshapes]
+    kd_max_depth: int = 13                 # KDtree::split(13) in Scene::loadObj (src/scene.cpp:868-872)
 
     def with_overrides(self, res=None, depth=None) -> "SceneDescription":
         import dataclasses
@@ -257,7 +264,7 @@ class SceneDescription:
             d.verts9, d.norms9, d.shape_of_tri = _fptr(v9), _fptr(n9), _iptr(st)
             d.num_shapes = len(sm)
             d.shape_materials = sm.ctypes.data_as(C.POINTER(Material))
-        d.kd_max_depth = 13
+        d.kd_max_depth = int(self.kd_max_depth)
         return d, keep
 
 
@@ -280,13 +287,23 @@ class SceneData:
         return cls(h)
 
     @classmethod
-    def from_description(cls, desc: SceneDescription) -> "SceneData":
+    def from_description(cls, desc: SceneDescription, kd_device: Optional[int] = None) -> "SceneData":
+        """kdpt_scene_build (host KD build), or kdpt_scene_build_device with the KD tree built on GPU
+        `kd_device` (byte-identical)."""
         lib = load_library()
         d, keep = desc.to_c()
         h = C.c_void_p()
-        _check(lib.kdpt_scene_build(C.byref(d), C.byref(h)), "kdpt_scene_build")
+        if kd_device is None:
+            _check(lib.kdpt_scene_build(C.byref(d), C.byref(h)), "kdpt_scene_build")
+        else:
+            _check(lib.kdpt_scene_build_device(C.byref(d), int(kd_device), C.byref(h)), "kdpt_scene_build_device")
         del keep
         return cls(h)
+
+    def kd_build_ms(self) -> float:
+        ms = C.c_double()
+        _check(load_library().kdpt_scene_kd_build_ms(self._h, C.byref(ms)), "kdpt_scene_kd_build_ms")
+        return float(ms.value)
 
     @property
     def resolution(self):
@@ -495,3 +512,22 @@ def imgsum(image: np.ndarray) -> float:
     im = np.asarray(image, dtype=np.float32).reshape(-1, 3)
     per_px = (im[:, 0] + im[:, 1]) + im[:, 2]  # float32 adds, left to right
     return float(np.sum(per_px.astype(np.float64)))
+
+
+def build_kd_device(verts9: np.ndarray, norms9: np.ndarray, mtl: np.ndarray, maxdepth: int = 13, device: int = 0):
+    """kdpt_build_kd_device over a triangle soup: (NodeBare bytes, TriBare bytes, build ms)."""
+    lib = load_library()
+    v = np.ascontiguousarray(verts9, np.float32).reshape(-1, 9)
+    n = np.ascontiguousarray(norms9, np.float32).reshape(-1, 9)
+    m = np.ascontiguousarray(mtl, np.int32).reshape(-1)
+    nodes, tris = C.c_void_p(), C.c_void_p()
+    nn, nt, ms = C.c_int(), C.c_int(), C.c_double()
+    _check(lib.kdpt_build_kd_device(_fptr(v), _fptr(n), _iptr(m), len(v), int(maxdepth), int(device), C.byref(nodes),
+                                    C.byref(nn), C.byref(tris), C.byref(nt), C.byref(ms)), "kdpt_build_kd_device")
+    try:
+        nb = C.string_at(nodes.value, 64 * nn.value) if nn.value else b""
+        tb = C.string_at(tris.value, 76 * nt.value) if nt.value else b""
+    finally:
+        lib.kdpt_free(nodes)
+        lib.kdpt_free(tris)
+    return nb, tb, float(ms.value)

@@ -53,7 +53,8 @@ def asan_host():
     exe = os.path.join(ROOT, "build", "asan_host")
     os.makedirs(os.path.dirname(exe), exist_ok=True)
     subprocess.run(["g++", *SAN, "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-I", os.path.join(ROOT, "include"),
-                    os.path.join(TESTS, "native", "asan_host.cpp"), os.path.join(CSRC, "scene_host.cpp"),
+                    os.path.join(TESTS, "native", "asan_host.cpp"), os.path.join(TESTS, "native", "no_device_build.cpp"),
+                    os.path.join(CSRC, "scene_host.cpp"),
                     os.path.join(CSRC, "image_io.cpp"), "-o", exe], check=True)
     return exe
 

@@ -9,5 +9,5 @@ mkdir -p "$ROOT/ab" "$ROOT/build/ab"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I "$ROOT/include" "$@" \
   -c "$ROOT/kdtreepathtraceroptimization_amd/csrc/kdpt_runtime.hip" -o "$ROOT/build/ab/$NAME.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/ab/$NAME.so" "$ROOT/build/ab/$NAME.o" \
-  "$ROOT/build/scene_host.o" "$ROOT/build/image_io.o"
+  "$ROOT/build/kd_build.o" "$ROOT/build/scene_host.o" "$ROOT/build/image_io.o"
 echo "ab/$NAME.so"
