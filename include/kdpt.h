@@ -283,6 +283,10 @@ typedef struct kdpt_scene_data kdpt_scene_data;
 int kdpt_scene_load(const char *scene_path, const char *obj_path, int res_w, int res_h, int depth,
                     kdpt_scene_data **out);
 
+/* kdpt_scene_load with the KD tree built on GPU `device` (byte-identical; see kdpt_scene_build_device). */
+int kdpt_scene_load_device(const char *scene_path, const char *obj_path, int res_w, int res_h, int depth,
+                           int device, kdpt_scene_data **out);
+
 /* The same from already-parsed values (what the parsers produce; fixtures use this). */
 typedef struct kdpt_scene_desc {
     int res[2];

@@ -68,6 +68,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--pipeline", type=int, default=8, help="batches in flight (throughput only)")
     ap.add_argument("--batch", type=int, default=4, help="iterations sharing an intersect launch (<= 4)")
+    ap.add_argument("--kd-build", choices=["gpu", "host"], default="gpu",
+                    help="build the KD tree on the GPU (default; byte-identical) or with the host recursion")
     ap.add_argument("--dry-run", action="store_true", help="load and build the scene, print it, render nothing")
     return ap.parse_args(argv)
 
@@ -88,11 +90,13 @@ def main(argv=None) -> int:
     iterations = a.iterations if a.iterations is not None else (hdr["iterations"] or 1)
     if iterations < 1:
         raise SystemExit("--iterations must be >= 1")
-    sd = SceneData.from_files(a.scene, a.mesh, res=tuple(a.res) if a.res else None, depth=a.depth)
+    kd_dev = a.device if (a.kd_build == "gpu" and not a.dry_run) else None  # --dry-run needs no GPU
+    sd = SceneData.from_files(a.scene, a.mesh, res=tuple(a.res) if a.res else None, depth=a.depth, kd_device=kd_dev)
     W, H = sd.resolution
     info = {"scene": a.scene, "mesh": a.mesh, "resolution": [W, H], "iterations": iterations,
             "geoms": sd.view.num_geoms, "materials": sd.view.num_materials, "kd_nodes": sd.view.num_nodes,
-            "kd_tri_refs": sd.view.num_tris}
+            "kd_tri_refs": sd.view.num_tris, "kd_build": a.kd_build if kd_dev is not None else "host",
+            "kd_build_ms": round(sd.kd_build_ms(), 3) if kd_dev is not None else None}
     if a.dry_run:
         print(json.dumps(info), flush=True)
         sd.close()

@@ -979,8 +979,9 @@ int kdpt_build_kd_device(const float* verts9, const float* norms9, const int* mt
 }
 
 
-int kdpt_scene_load(const char* scene_path, const char* obj_path, int res_w, int res_h, int depth,
-                    kdpt_scene_data** out) {
+namespace {
+int scene_load(const char* scene_path, const char* obj_path, int res_w, int res_h, int depth, int device,
+               kdpt_scene_data** out) {
   if (!scene_path || !out) return KDPT_ERR_ARG;
   ParsedScene ps;
   int rc = parse_scene_text(scene_path, ps);
@@ -1011,7 +1012,19 @@ int kdpt_scene_load(const char* scene_path, const char* obj_path, int res_w, int
   d.shape_of_tri = soup.shape.data();
   d.num_shapes = (int)soup.shape_mats.size();
   d.shape_materials = soup.shape_mats.data();
-  return kdpt_scene_build(&d, out);
+  return scene_build(&d, device, out);
+}
+}  // namespace
+
+int kdpt_scene_load(const char* scene_path, const char* obj_path, int res_w, int res_h, int depth,
+                    kdpt_scene_data** out) {
+  return scene_load(scene_path, obj_path, res_w, res_h, depth, -1, out);
+}
+
+int kdpt_scene_load_device(const char* scene_path, const char* obj_path, int res_w, int res_h, int depth, int device,
+                           kdpt_scene_data** out) {
+  if (device < 0) return KDPT_ERR_ARG;
+  return scene_load(scene_path, obj_path, res_w, res_h, depth, device, out);
 }
 
 int kdpt_scene_view(const kdpt_scene_data* sd, kdpt_scene* o) {

@@ -113,7 +113,7 @@ EXPORTS = [
     "kdpt_selftest_fresnel", "kdpt_selftest_libm", "kdpt_selftest_libm_digest", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
     "kdpt_save_rgb8", "kdpt_save_png", "kdpt_save_hdr", "kdpt_png_encode", "kdpt_write_png", "kdpt_hdr_encode",
     "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm", "kdpt_set_options", "kdpt_scene_build_device",
-    "kdpt_scene_kd_build_ms", "kdpt_build_kd_device",
+    "kdpt_scene_kd_build_ms", "kdpt_build_kd_device", "kdpt_scene_load_device",
 ]
 
 _lib = None
@@ -174,6 +174,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     if hasattr(lib, "kdpt_scene_build_device"):
         lib.kdpt_scene_build_device.argtypes = [P(SceneDesc), C.c_int, P(C.c_void_p)]
         lib.kdpt_scene_kd_build_ms.argtypes = [C.c_void_p, P(C.c_double)]
+        lib.kdpt_scene_load_device.argtypes = [C.c_char_p, C.c_char_p, C.c_int, C.c_int, C.c_int, C.c_int,
+                                               P(C.c_void_p)]
         lib.kdpt_build_kd_device.argtypes = [P(C.c_float), P(C.c_float), P(C.c_int), C.c_int, C.c_int, C.c_int,
                                              P(C.c_void_p), P(C.c_int), P(C.c_void_p), P(C.c_int), P(C.c_double)]
     if hasattr(lib, "kdpt_set_options"):
@@ -277,12 +279,18 @@ class SceneData:
         _check(load_library().kdpt_scene_view(self._h, C.byref(self.view)), "kdpt_scene_view")
 
     @classmethod
-    def from_files(cls, scene_path: str, obj_path: Optional[str] = None, res=None, depth=None) -> "SceneData":
+    def from_files(cls, scene_path: str, obj_path: Optional[str] = None, res=None, depth=None,
+                   kd_device: Optional[int] = None) -> "SceneData":
+        """kdpt_scene_load (host KD build) or kdpt_scene_load_device (KD tree built on GPU kd_device)."""
         lib = load_library()
         h = C.c_void_p()
         w, hh = (res if res is not None else (0, 0))
-        rc = lib.kdpt_scene_load(scene_path.encode(), obj_path.encode() if obj_path else None, int(w), int(hh),
-                                 int(depth or 0), C.byref(h))
+        if kd_device is None:
+            rc = lib.kdpt_scene_load(scene_path.encode(), obj_path.encode() if obj_path else None, int(w), int(hh),
+                                     int(depth or 0), C.byref(h))
+        else:
+            rc = lib.kdpt_scene_load_device(scene_path.encode(), obj_path.encode() if obj_path else None, int(w),
+                                            int(hh), int(depth or 0), int(kd_device), C.byref(h))
         _check(rc, f"kdpt_scene_load({scene_path}, {obj_path})")
         return cls(h)
 
