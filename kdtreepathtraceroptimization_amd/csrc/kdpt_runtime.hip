@@ -926,35 +926,41 @@ __device__ inline unsigned long long lb_pack(unsigned long long flag, unsigned s
   return (flag << 62) | ((unsigned long long)s << 31) | (unsigned long long)w;
 }
 
-// STAGE: the analytic geoms and the materials copied into LDS first (small scenes: their per-lane reads,
-// indexed by hit and by nearest-first order, are then LDS reads instead of L2 round trips)
 constexpr int STAGE_MATS = 32;
-template <bool HYBRID, bool STAGE>
-__global__ __launch_bounds__(TILE) void k_shade_fused(ShadeArgs A, FuseArgs F) {
-  const int n = A.counts[A.depth];
-  __shared__ int s_tile;
-  __shared__ unsigned s_cnt[2][TILE / 64];
-  __shared__ unsigned s_ex[2];
+
+// The LDS a shading workgroup uses: staged geoms/materials and the per-tile compaction scratch.
+template <bool STAGE>
+struct ShadeLDS {
+  int tile, b;
+  unsigned cnt[2][TILE / 64];
+  unsigned ex[2];
+  uint32_t geoms[STAGE ? ORDERED_GEOMS * sizeof(DevGeom) / 4 : 1];
+  uint32_t mats[STAGE ? STAGE_MATS * sizeof(DevMaterial) / 4 : 1];
+};
+
+// STAGE: the analytic geoms and the materials copied into LDS (small scenes: their per-lane reads, indexed
+// by hit and by nearest-first order, are then LDS reads instead of L2 round trips)
+template <bool STAGE>
+__device__ __attribute__((always_inline)) inline DevScene stage_scene(const DevScene& S0, ShadeLDS<STAGE>& L) {
   static_assert(sizeof(DevGeom) % 4 == 0 && sizeof(DevMaterial) % 4 == 0, "staged as dwords");
-  __shared__ uint32_t s_geoms[STAGE ? ORDERED_GEOMS * sizeof(DevGeom) / 4 : 1];
-  __shared__ uint32_t s_mats[STAGE ? STAGE_MATS * sizeof(DevMaterial) / 4 : 1];
-  if (threadIdx.x == 0) s_tile = atomicAdd(&F.tickets[A.depth], 1);
-  __syncthreads();
-  const int tile = s_tile;
-  // uniform per block; the grid covers every pixel, so past the first bounces most blocks leave here,
-  // before staging anything
-  if (tile * TILE >= n) return;
+  DevScene S = S0;
   if (STAGE) {
-    const int gw = A.S.num_geoms * (int)(sizeof(DevGeom) / 4), mw = A.S.num_materials * (int)(sizeof(DevMaterial) / 4);
-    for (int k = threadIdx.x; k < gw; k += TILE) s_geoms[k] = reinterpret_cast<const uint32_t*>(A.S.geoms)[k];
-    for (int k = threadIdx.x; k < mw; k += TILE) s_mats[k] = reinterpret_cast<const uint32_t*>(A.S.materials)[k];
+    const int gw = S0.num_geoms * (int)(sizeof(DevGeom) / 4), mw = S0.num_materials * (int)(sizeof(DevMaterial) / 4);
+    for (int k = threadIdx.x; k < gw; k += TILE) L.geoms[k] = reinterpret_cast<const uint32_t*>(S0.geoms)[k];
+    for (int k = threadIdx.x; k < mw; k += TILE) L.mats[k] = reinterpret_cast<const uint32_t*>(S0.materials)[k];
     __syncthreads();
+    S.geoms = reinterpret_cast<const DevGeom*>(L.geoms);
+    S.materials = reinterpret_cast<const DevMaterial*>(L.mats);
   }
-  DevScene S = A.S;
-  if (STAGE) {
-    S.geoms = reinterpret_cast<const DevGeom*>(s_geoms);
-    S.materials = reinterpret_cast<const DevMaterial*>(s_mats);
-  }
+  return S;
+}
+
+// One 256-path tile of one iteration: shading, the survivors' stable compaction into the other path buffer
+// (decoupled look-back over the earlier tiles' records), the next bounce's intersect-stage hand-off.  Tiles
+// of an iteration must be started in increasing order (tickets), so every earlier tile is already running.
+template <bool HYBRID, bool STAGE>
+__device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs& A, const FuseArgs& F, const DevScene& S, int tile, int n,
+                                  ShadeLDS<STAGE>& L) {
   const int i = tile * TILE + threadIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
   if (i == 0) shade_stats(A, n);
@@ -964,15 +970,15 @@ __global__ __launch_bounds__(TILE) void k_shade_fused(ShadeArgs A, FuseArgs F) {
   const unsigned long long ms = __ballot(o.alive), mw = __ballot(o.walk);
   if (A.count_aabb && A.prep_on) count_prep(A, o.tested, o.walk);
   if (lane == 0) {
-    s_cnt[0][wid] = (unsigned)__popcll(ms);
-    s_cnt[1][wid] = (unsigned)__popcll(mw);
+    L.cnt[0][wid] = (unsigned)__popcll(ms);
+    L.cnt[1][wid] = (unsigned)__popcll(mw);
   }
   __syncthreads();
   if (wid == 0) {
     unsigned aS = 0, aW = 0;
     for (int w = 0; w < TILE / 64; w++) {
-      aS += s_cnt[0][w];
-      aW += s_cnt[1][w];
+      aS += L.cnt[0][w];
+      aW += L.cnt[1][w];
     }
     unsigned long long* lb = F.lb + (size_t)A.depth * A.ntiles;
     unsigned eS = 0, eW = 0;
@@ -1002,8 +1008,8 @@ __global__ __launch_bounds__(TILE) void k_shade_fused(ShadeArgs A, FuseArgs F) {
       if (lane == 0) lb_store(lb + tile, lb_pack(2, eS + aS, eW + aW));
     }
     if (lane == 0) {
-      s_ex[0] = eS;
-      s_ex[1] = eW;
+      L.ex[0] = eS;
+      L.ex[1] = eW;
       if (tile == (n - 1) / TILE) {  // the last tile: the next bounce's path and candidate counts
         F.counts[A.depth + 1] = (int)(eS + aS);
         if (A.prep_on) F.ccount[A.depth + 1] = (int)(eW + aW);
@@ -1012,10 +1018,10 @@ __global__ __launch_bounds__(TILE) void k_shade_fused(ShadeArgs A, FuseArgs F) {
   }
   __syncthreads();
   if (o.alive) {
-    unsigned bS = s_ex[0], bW = s_ex[1];
+    unsigned bS = L.ex[0], bW = L.ex[1];
     for (int w = 0; w < wid; w++) {
-      bS += s_cnt[0][w];
-      bW += s_cnt[1][w];
+      bS += L.cnt[0][w];
+      bW += L.cnt[1][w];
     }
     const int d = (int)(bS + lane_prefix(ms));
     F.dst.p0[d] = o.q0;
@@ -1031,6 +1037,21 @@ __global__ __launch_bounds__(TILE) void k_shade_fused(ShadeArgs A, FuseArgs F) {
       }
     }
   }
+}
+
+// One launch per bounce and iteration: tile = ticket (tickets start the tiles in order).
+template <bool HYBRID, bool STAGE>
+__global__ __launch_bounds__(TILE) void k_shade_fused(ShadeArgs A, FuseArgs F) {
+  const int n = A.counts[A.depth];
+  // the grid covers every pixel, so past the first bounces most workgroups have no tile: exactly the first
+  // ceil(n / TILE) take tickets (one contended atomic per tile, not per workgroup), the rest leave at once
+  if ((int)blockIdx.x * TILE >= n) return;
+  __shared__ ShadeLDS<STAGE> L;
+  if (threadIdx.x == 0) L.tile = atomicAdd(&F.tickets[A.depth], 1);
+  __syncthreads();
+  const int tile = L.tile;
+  const DevScene S = stage_scene<STAGE>(A.S, L);
+  shade_tile<HYBRID, STAGE>(A, F, S, tile, n, L);
 }
 
 // Exclusive scan of the tile counts (one workgroup; <= MAX_KEYS * ntiles entries).
