@@ -496,8 +496,8 @@ struct ClustersInterleaved {
 };
 
 struct WaveLeafLDS {
-  int pend[64];    // inclusive end of each lane's pair range
-  int tbase[64];   // triangle index = tbase[owner] + pair index
+  int slot[64];    // pair_owner's scatter slots (all zero between calls)
+  int tbase[64];   // item (cluster / triangle) index = tbase[owner] + pair index
   float4 od[64];   // ray origin.xyz, direction.x
   float2 dd[64];   // direction.y, direction.z
   unsigned long long lastPass[64];  // ((tri + 1) << 32) | bary.z bits, max
@@ -550,6 +550,23 @@ __device__ inline unsigned long long lane63_u64(unsigned long long v) {
 #define KDPT_WAVE_REDUCE(STEP) STEP(0xB1, 0xF) STEP(0x4E, 0xF) STEP(0x141, 0xF) STEP(0x140, 0xF) \
                                STEP(0x142, 0xA) STEP(0x143, 0xC)
 
+// Inclusive prefix sum / max over the wave on DPP row shifts and row broadcasts (VALU only): shr 1, 2, 4, 8
+// within each 16-lane row, then row_bcast:15 (rows 1, 3) and row_bcast:31 (rows 2, 3) carry the rows below.
+// Lanes whose source is outside the row, or rows the row mask leaves out, add the identity 0 (values >= 0
+// for the max).  Every lane of the wave must be active.
+template <bool MAX>
+__device__ inline int wave_incl_scan(int v) {
+#define KDPT_SCAN(C, R)                                                   \
+  {                                                                       \
+    const int o = __builtin_amdgcn_update_dpp(0, v, C, R, 0xF, false);    \
+    v = MAX ? max(v, o) : v + o;                                          \
+  }
+  KDPT_SCAN(0x111, 0xF) KDPT_SCAN(0x112, 0xF) KDPT_SCAN(0x114, 0xF) KDPT_SCAN(0x118, 0xF)
+  KDPT_SCAN(0x142, 0xA) KDPT_SCAN(0x143, 0xC)
+#undef KDPT_SCAN
+  return v;
+}
+
 __device__ inline unsigned long long wave_min_u64(unsigned long long v) {
 #define KDPT_STEP(C, R) { const unsigned long long o = dpp_u64<C, R>(v); v = o < v ? o : v; }
   KDPT_WAVE_REDUCE(KDPT_STEP)
@@ -589,6 +606,29 @@ __device__ inline void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
   __builtin_amdgcn_wave_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+__device__ inline float bpermute_f(float v, int src_lane) {
+  return __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane << 2, __float_as_int(v)));
+}
+
+// Owner lane of pair B + lane in a flattened (lane, item) enumeration where lane L owns pairs
+// [excl_L, excl_L + cnt_L) (lanes in order, so starts increase with L).  The segment starts inside the
+// window [B, B + 64) are scattered into slot[] (lane + 1), an inclusive max-scan fills the gaps, and a
+// window position no start precedes belongs to the previous window's last owner (carry, updated).  Replaces
+// a 6-step binary search (6 dependent LDS reads) by one LDS round trip plus DPP.  Wave-uniform call; slot[]
+// is all zero on entry and on exit.
+__device__ inline int pair_owner(int* slot, int excl, int cnt, int B, int& carry) {
+  const int lane = threadIdx.x & 63;
+  const int rel = excl - B;
+  const bool mine = cnt > 0 && rel >= 0 && rel < 64;
+  if (mine) slot[rel] = lane + 1;
+  wave_lds_sync();
+  const int v = wave_incl_scan<true>(slot[lane]);
+  if (mine) slot[rel] = 0;  // after the read above (same wave: LDS operations stay in order)
+  const int own = v > 0 ? v - 1 : carry;
+  carry = __builtin_amdgcn_readlane(own, 63);
+  return own;
 }
 
 __device__ inline TriData tri_load(const DevScene& S, int i) { return TriData{S.tv0[i], S.te1[i], S.te2[i]}; }
@@ -774,113 +814,116 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   float r_bz = 0.0f;
   int r_lasthit = -1, r_nhit = 0;
   unsigned long long r_best = ~0ull;
-  // (a) big leaves: the whole wave sweeps one leaf at a time with a uniform ray
+  // Both leaf kinds enumerate (lane, item) pairs flattened over the wave: lane L owns pairs
+  // [excl_L, excl_L + count_L), and lane k of a round takes pair B + k, whichever ray it belongs to.
+  // (a) big leaves: the items are 64-triangle clusters.  One pass culls 64 (ray, cluster) pairs (clusters
+  // whose box the ray's line misses, when every invdir is finite); each surviving cluster is then swept by
+  // the whole wave with its ray, 64 triangles at a time, the next survivor's triangles fetched while this
+  // one is tested.  Recombination by ORIGINAL index into the owner lane (order-free): last u/v pass = max
+  // index, last hit = max, best = min (t, index).
   const bool big = leaf && lsize >= BIG_LEAF;
-  unsigned long long bigmask = __ballot(big);
-  while (bigmask) {
-    // One big leaf at a time, the whole wave on it with that lane's ray: clusters whose box the
-    // ray's line misses are skipped (when every invdir is finite), the others tested 64 at a time.
-    // Recombination by ORIGINAL index: last u/v pass = max index, last hit = max, best = min (t, index).
-    const int j = __builtin_ctzll(bigmask);
-    bigmask &= bigmask - 1;
-    const int jfirst = NodeSrc::kLeafHoldsCluster ? __builtin_amdgcn_readlane(lstart, j)
-                                                  : S.leaf_cl[__builtin_amdgcn_readlane(lnode, j)].x;
-    const int jcount = (__builtin_amdgcn_readlane(lsize, j) + 63) >> 6;
-    // lane j's ray, wave-uniform: read into scalar registers
-    const f3 jo = mk3(readlane_f(o.x, j), readlane_f(o.y, j), readlane_f(o.z, j));
-    const f3 jd = mk3(readlane_f(d.x, j), readlane_f(d.y, j), readlane_f(d.z, j));
-    const f3 jinv = mk3(readlane_f(invdir.x, j), readlane_f(invdir.y, j), readlane_f(invdir.z, j));
-    const int2 cr = make_int2(jfirst, jcount);
+  if (__any(big)) {
+    const int ncl = big ? (lsize + 63) >> 6 : 0;
+    const int cfirst = big ? (NodeSrc::kLeafHoldsCluster ? lstart : S.leaf_cl[lnode].x) : 0;
+    const int incl = wave_incl_scan<false>(ncl);
+    const int P = __builtin_amdgcn_readlane(incl, 63);
+    const int excl = incl - ncl;
+    W->tbase[lane] = cfirst - excl;  // cluster of pair q = tbase[owner] + q
+    wave_lds_sync();
     if (COUNT) {
-      prof_add(W, PROF_BIG_LEAVES, 1);
-      prof_add(W, PROF_BIG_CLUSTERS, (unsigned long long)jcount);
+      prof_add(W, PROF_BIG_LEAVES, (unsigned long long)__popcll(__ballot(big)));
+      prof_add(W, PROF_BIG_CLUSTERS, (unsigned long long)P);
     }
-    unsigned long long u_pass = 0ull, u_best = ~0ull;
-    int u_lasthit = -1, u_nhit = 0;
-    for (int cb0 = 0; cb0 < cr.y; cb0 += 64) {
-     // lane k culls cluster cb0 + k: one parallel pass over the boxes, then only the survivors
-     const int ck = cr.x + cb0 + lane;
-     const bool cv = cb0 + lane < cr.y;
-     const int cq = cv ? ck : cr.x;
-     unsigned long long cmask =
-         __ballot(cv && (!fastAABB || cluster_may_pass(clusters.lo_of(cq), clusters.hi_of(cq), jo, jinv)));
-     // clusters are padded to 64 entries (padding never passes: e1 = e2 = 0), so cluster c's triangles
-     // are c*64 + lane; the next surviving cluster's triangles are fetched while this one is tested
-     int c = -1;
-     TriData T{};
-     if (cmask) {
-       c = cr.x + cb0 + __builtin_ctzll(cmask);
-       cmask &= cmask - 1;
-       const int ct = c * 64 + lane;
-       T = TriData{S.c_v0[ct], S.c_e1[ct], S.c_e2[ct]};
-     }
-     while (c >= 0) {
-      int cn = -1;
-      TriData Tn{};
-      if (cmask) {
-        cn = cr.x + cb0 + __builtin_ctzll(cmask);
-        cmask &= cmask - 1;
-        const int ctn = cn * 64 + lane;
-        Tn = TriData{S.c_v0[ctn], S.c_e1[ctn], S.c_e2[ctn]};
+    unsigned long long k_pass = 0ull, k_best = ~0ull;
+    int k_lasthit = -1, k_nhit = 0;
+    int carry = 0;
+    for (int B = 0; B < P; B += 64) {
+      const int own = pair_owner(W->slot, excl, ncl, B, carry);
+      const int c = W->tbase[own] + B + lane;
+      bool pass = B + lane < P;
+      if (fastAABB) {
+        const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
+        const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
+        if (pass) pass = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
       }
-      if (COUNT) prof_add(W, PROF_BIG_SWEEPS, 1);
-      const int orig = fbits(T.e1.w);
-      float bx = 0, by = 0, bzk = 0;
-      const int r = tri_test_v(T, jo, jd, bx, by, bzk);
-      const unsigned long long m1 = __ballot(r >= 1);
-      if (COUNT && m1) {
-        prof_add(W, PROF_BIG_PASS, 1);
-        prof_add(W, PROF_BIG_MULTI, (m1 & (m1 - 1)) ? 1 : 0);
+      unsigned long long sm = __ballot(pass);
+      int s = -1;
+      TriData T{};
+      if (sm) {
+        s = __builtin_ctzll(sm);
+        sm &= sm - 1;
+        const int ct = __builtin_amdgcn_readlane(c, s) * 64 + lane;
+        T = TriData{S.c_v0[ct], S.c_e1[ct], S.c_e2[ct]};
       }
-      if (m1) {
-        const unsigned long long pk =
-            r >= 1 ? ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk) : 0ull;
-        // usually one lane of the cluster passes: read its key instead of reducing over the wave
-        const unsigned long long wm = (m1 & (m1 - 1)) == 0ull ? readlane_u64(pk, __builtin_ctzll(m1))
-                                                              : wave_max_u64(pk);
-        u_pass = wm > u_pass ? wm : u_pass;
-        const unsigned long long m2 = __ballot(r == 2);
-        if (m2) {
-          const bool one = (m2 & (m2 - 1)) == 0ull;
-          const int jh = __builtin_ctzll(m2);
-          u_nhit += __builtin_popcountll(m2);
-          u_lasthit = max(u_lasthit, one ? __builtin_amdgcn_readlane(orig, jh) : wave_max_i32(r == 2 ? orig : -1));
-          unsigned long long key = ~0ull;
-          if (r == 2) {
-            f3 hp, nn;
-            const float t = tri_hit_t<HYBRID>(S, orig, jo, jd, bx, by, bzk, hp, nn);
-            if (t > 0.0f) key = ((unsigned long long)f2u(t) << 32) | (unsigned int)orig;
-          }
-          const unsigned long long wb = one ? readlane_u64(key, jh) : wave_min_u64(key);
-          u_best = wb < u_best ? wb : u_best;
+      while (s >= 0) {
+        int sn = -1;
+        TriData Tn{};
+        if (sm) {
+          sn = __builtin_ctzll(sm);
+          sm &= sm - 1;
+          const int ctn = __builtin_amdgcn_readlane(c, sn) * 64 + lane;
+          Tn = TriData{S.c_v0[ctn], S.c_e1[ctn], S.c_e2[ctn]};
         }
+        if (COUNT) prof_add(W, PROF_BIG_SWEEPS, 1);
+        const int j = __builtin_amdgcn_readlane(own, s);  // the cluster's ray: lane j's, wave-uniform
+        const f3 jo = mk3(readlane_f(o.x, j), readlane_f(o.y, j), readlane_f(o.z, j));
+        const f3 jd = mk3(readlane_f(d.x, j), readlane_f(d.y, j), readlane_f(d.z, j));
+        const int orig = fbits(T.e1.w);
+        float bx = 0, by = 0, bzk = 0;
+        const int r = tri_test_v(T, jo, jd, bx, by, bzk);
+        const unsigned long long m1 = __ballot(r >= 1);
+        if (COUNT && m1) {
+          prof_add(W, PROF_BIG_PASS, 1);
+          prof_add(W, PROF_BIG_MULTI, (m1 & (m1 - 1)) ? 1 : 0);
+        }
+        if (m1) {
+          const unsigned long long pk =
+              r >= 1 ? ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk) : 0ull;
+          // usually one lane of the cluster passes: read its key instead of reducing over the wave
+          const unsigned long long wm = (m1 & (m1 - 1)) == 0ull ? readlane_u64(pk, __builtin_ctzll(m1))
+                                                                : wave_max_u64(pk);
+          if (lane == j) k_pass = wm > k_pass ? wm : k_pass;
+          const unsigned long long m2 = __ballot(r == 2);
+          if (m2) {
+            const bool one = (m2 & (m2 - 1)) == 0ull;
+            const int jh = __builtin_ctzll(m2);
+            const int lh = one ? __builtin_amdgcn_readlane(orig, jh) : wave_max_i32(r == 2 ? orig : -1);
+            unsigned long long key = ~0ull;
+            if (r == 2) {
+              f3 hp, nn;
+              const float t = tri_hit_t<HYBRID>(S, orig, jo, jd, bx, by, bzk, hp, nn);
+              if (t > 0.0f) key = ((unsigned long long)f2u(t) << 32) | (unsigned int)orig;
+            }
+            const unsigned long long wb = one ? readlane_u64(key, jh) : wave_min_u64(key);
+            if (lane == j) {
+              k_nhit += __builtin_popcountll(m2);
+              k_lasthit = max(k_lasthit, lh);
+              k_best = wb < k_best ? wb : k_best;
+            }
+          }
+        }
+        s = sn;
+        T = Tn;
       }
-      c = cn;
-      T = Tn;
-     }
     }
-    if (lane == j) {
-      r_pass = (int)(u_pass >> 32);
-      r_bz = u2f((uint32_t)(u_pass & 0xffffffffu));
-      r_lasthit = u_lasthit;
-      r_nhit = u_nhit;
-      r_best = u_best;
+    if (big) {
+      r_pass = (int)(k_pass >> 32);
+      r_bz = u2f((uint32_t)(k_pass & 0xffffffffu));
+      r_lasthit = k_lasthit;
+      r_nhit = k_nhit;
+      r_best = k_best;
     }
   }
   if (COUNT) prof_lap(W, PROF_BIG_CYC);
-  // (b) small leaves: all (ray, triangle) pairs spread over the 64 lanes
+  // (b) small leaves: the items are triangles, every (ray, triangle) pair tested by one lane; results
+  // recombine through LDS atomics on the owner's slots
   const int sz = (leaf && !big) ? lsize : 0;
   if (__any(sz > 0)) {
     if (COUNT) prof_add(W, PROF_SMALL_PHASES, 1);
-    int incl = sz;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const int y = __shfl_up(incl, off);
-      if (lane >= off) incl += y;
-    }
-    const int P = __shfl(incl, 63);
-    W->pend[lane] = incl;
-    W->tbase[lane] = lstart - (incl - sz);
+    const int incl = wave_incl_scan<false>(sz);
+    const int P = __builtin_amdgcn_readlane(incl, 63);
+    const int excl = incl - sz;
+    W->tbase[lane] = lstart - excl;  // triangle of pair q = tbase[owner] + q
     W->lastPass[lane] = 0ull;
     W->lastHit[lane] = -1;
     W->nhit[lane] = 0;
@@ -890,47 +933,36 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       prof_add(W, PROF_SMALL_ROUNDS, (unsigned long long)((P + 63) / 64));
       prof_add(W, PROF_SMALL_PAIRS, (unsigned long long)P);
     }
-    // pair pi -> owner lane (binary search over the inclusive ends) and triangle; the next
-    // round's pair is located and its triangle loaded while the current one is tested
-    auto owner_of = [&](int q) {
-      int lo = 0, hi = 63;
-#pragma unroll
-      for (int st = 0; st < 6; st++) {
-        const int mid = (lo + hi) >> 1;
-        if (W->pend[mid] > q) hi = mid; else lo = mid + 1;
-      }
-      return lo;
-    };
-    int pi = lane;
-    int owner = 0, tri = 0;
+    // the next round's owners are found and its triangles loaded while the current round is tested
+    int carry = 0;
+    int owner = pair_owner(W->slot, excl, sz, 0, carry);
+    int tri = W->tbase[owner] + lane;
     TriData nxt{};
-    if (pi < P) {
-      owner = owner_of(pi);
-      tri = W->tbase[owner] + pi;
-      nxt = tri_load(S, tri);
-    }
-    while (pi < P) {
+    if (lane < P) nxt = tri_load(S, tri);
+    for (int B = 0; B < P; B += 64) {
       const TriData cur_t = nxt;
       const int cowner = owner, ctri = tri;
-      pi += 64;
-      if (pi < P) {
-        owner = owner_of(pi);
-        tri = W->tbase[owner] + pi;
-        nxt = tri_load(S, tri);
+      const bool valid = B + lane < P;
+      if (B + 64 < P) {
+        owner = pair_owner(W->slot, excl, sz, B + 64, carry);
+        tri = W->tbase[owner] + B + 64 + lane;
+        if (B + 64 + lane < P) nxt = tri_load(S, tri);
       }
-      const float4 q0 = W->od[cowner];
-      const float2 q1 = W->dd[cowner];
-      const f3 oo = mk3(q0.x, q0.y, q0.z), dd = mk3(q0.w, q1.x, q1.y);
-      float bx, by, bzk;
-      const int r = tri_test_v(cur_t, oo, dd, bx, by, bzk);
-      if (r >= 1)
-        atomicMax(&W->lastPass[cowner], ((unsigned long long)(unsigned int)(ctri + 1) << 32) | f2u(bzk));
-      if (r == 2) {
-        atomicMax(&W->lastHit[cowner], ctri);
-        atomicAdd(&W->nhit[cowner], 1);
-        f3 hp, nn;
-        const float t = tri_hit_t<HYBRID>(S, ctri, oo, dd, bx, by, bzk, hp, nn);
-        if (t > 0.0f) atomicMin(&W->best[cowner], ((unsigned long long)f2u(t) << 32) | (unsigned int)ctri);
+      if (valid) {
+        const float4 q0 = W->od[cowner];
+        const float2 q1 = W->dd[cowner];
+        const f3 oo = mk3(q0.x, q0.y, q0.z), dd = mk3(q0.w, q1.x, q1.y);
+        float bx, by, bzk;
+        const int r = tri_test_v(cur_t, oo, dd, bx, by, bzk);
+        if (r >= 1)
+          atomicMax(&W->lastPass[cowner], ((unsigned long long)(unsigned int)(ctri + 1) << 32) | f2u(bzk));
+        if (r == 2) {
+          atomicMax(&W->lastHit[cowner], ctri);
+          atomicAdd(&W->nhit[cowner], 1);
+          f3 hp, nn;
+          const float t = tri_hit_t<HYBRID>(S, ctri, oo, dd, bx, by, bzk, hp, nn);
+          if (t > 0.0f) atomicMin(&W->best[cowner], ((unsigned long long)f2u(t) << 32) | (unsigned int)ctri);
+        }
       }
     }
     wave_lds_sync();

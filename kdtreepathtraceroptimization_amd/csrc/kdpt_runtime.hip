@@ -367,6 +367,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
   WaveLeafLDS* W = &s_leaf[threadIdx.x >> 6];
   if (COUNT && lane < PROF_SLOTS) W->prof[lane] = 0;
   if (COUNT && lane == 0) W->tail_t0 = 0;
+  W->slot[lane] = 0;  // pair_owner's invariant
   // launch duration on the device clock (first block start .. last block end); the HIP events around
   // the launch also count time spent queued behind other streams' kernels when iterations overlap
   __shared__ int s_waves_done;
