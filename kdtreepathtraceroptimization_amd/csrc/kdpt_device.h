@@ -214,8 +214,17 @@ __device__ inline bool intersectAABB_fast(f3 o, f3 invdir, float4 b0, float4 b1,
   const float v1 = (b0.x - o.x) * invdir.x, v2 = (b0.w - o.x) * invdir.x;
   const float v3 = (b0.y - o.y) * invdir.y, v4 = (b1.x - o.y) * invdir.y;
   const float v5 = (b0.z - o.z) * invdir.z, v6 = (b1.y - o.z) * invdir.z;
-  const float dmin = fmaxf(fmaxf(fminf(v1, v2), fminf(v3, v4)), fminf(v5, v6));
-  const float dmax = fminf(fminf(fmaxf(v1, v2), fmaxf(v3, v4)), fmaxf(v5, v6));
+  // v_min/v_max straight from the products: the compiler's fminf/fmaxf would first quiet each input
+  // (six v_max x, x, x per node step) although a product is never a signalling NaN
+  float l1, l2, l3, h1, h2, h3, dmin, dmax;
+  asm("v_min_f32 %0, %1, %2" : "=v"(l1) : "v"(v1), "v"(v2));
+  asm("v_min_f32 %0, %1, %2" : "=v"(l2) : "v"(v3), "v"(v4));
+  asm("v_min_f32 %0, %1, %2" : "=v"(l3) : "v"(v5), "v"(v6));
+  asm("v_max_f32 %0, %1, %2" : "=v"(h1) : "v"(v1), "v"(v2));
+  asm("v_max_f32 %0, %1, %2" : "=v"(h2) : "v"(v3), "v"(v4));
+  asm("v_max_f32 %0, %1, %2" : "=v"(h3) : "v"(v5), "v"(v6));
+  asm("v_max3_f32 %0, %1, %2, %3" : "=v"(dmin) : "v"(l1), "v"(l2), "v"(l3));
+  asm("v_min3_f32 %0, %1, %2, %3" : "=v"(dmax) : "v"(h1), "v"(h2), "v"(h3));
   dist = dmin;
   return !(dmax < 0.0f) && !(dmin > dmax);
 }
@@ -431,7 +440,8 @@ __device__ inline int trace_class(const DevScene& S, f3 o, f3 d) {
 struct NodeRec {
   float4 b0;     // min.xyz, max.x
   float4 b1;     // max.y, max.z, -, -
-  int left, right, parent, axis, triStart, triSize;
+  int left, right, parent, axis, triStart, triSize;  // left / right: child index when hasL / hasR
+  bool hasL, hasR;
 };
 
 struct NodesWide {
@@ -444,6 +454,8 @@ struct NodesWide {
     r.b1 = make_float4(ibits(q1.x), ibits(q1.y), 0.0f, 0.0f);
     r.left = q1.z;
     r.right = q1.w;
+    r.hasL = q1.z != -1;
+    r.hasR = q1.w != -1;
     r.parent = q2.x;
     r.triStart = q2.y;
     r.triSize = q2.z;
@@ -464,8 +476,10 @@ struct NodesPacked {
     r.b1 = make_float4(ibits(q1.x), ibits(q1.y), 0.0f, 0.0f);
     const uint32_t w6 = (uint32_t)q1.z, w7 = (uint32_t)q1.w;
     const bool tris = (w7 >> 18) & 1u;
-    r.left = tris ? -1 : link16(w6 & 0xffffu);
-    r.right = tris ? -1 : link16(w6 >> 16);
+    r.left = (int)(w6 & 0xffffu);  // raw: only read when hasL / hasR
+    r.right = (int)(w6 >> 16);
+    r.hasL = !tris && (w6 & 0xffffu) != 0xffffu;
+    r.hasR = !tris && (w6 >> 16) != 0xffffu;
     r.parent = link16(w7 & 0xffffu);
     r.axis = (int)((w7 >> 16) & 3u);
     r.triStart = (int)w6;
@@ -729,6 +743,8 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   enum : uint32_t { F_ROOTV = 1, F_SINK = 2, F_HITGEOM = 4, F_DONE = 8, F_LEAF = 16, F_LFIRST = 32, F_FAULT = 64 };
   uint32_t fl = (rootv ? F_ROOTV : 0u) | (sink ? F_SINK : 0u) | (hitGeom ? F_HITGEOM : 0u) | (done ? F_DONE : 0u) |
                 F_LFIRST;
+  // leftFirst = d[axis] > 0 (comp: axis 0, 1, anything else z) as one bit test per trip
+  const uint32_t dpos = (d.x > 0.0f ? 1u : 0u) | (d.y > 0.0f ? 2u : 0u) | (d.z > 0.0f ? 4u : 0u);
   while (true) {
     const bool walk = (fl & (F_DONE | F_LEAF)) == 0u;
     const unsigned long long wmask = __ballot(walk);
@@ -754,12 +770,13 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     const bool hg = fastAABB ? intersectAABB_fast(o, invdir, nd.b0, nd.b1, dd)
                              : intersectAABB(o, invdir, nd.b0, nd.b1, dd);
     const bool up = curVis || !hg || dd > bz;
-    const bool leftFirst = HYBRID ? (comp(d, nd.axis) > 0.0f) : true;
+    const bool leftFirst = HYBRID ? ((dpos >> min((uint32_t)nd.axis, 2u)) & 1u) != 0u : true;
     const uint32_t fside = leftFirst ? 0u : 1u;
     const uint32_t cl = (cb >> ((2u * Lu) & 31u)) & 3u;  // child flags of this level
     const int first = leftFirst ? left : right, second = leftFirst ? right : left;
-    const bool takeFirst = first != -1 && !((cl >> fside) & 1u);
-    const bool takeSecond = second != -1 && !((cl >> (fside ^ 1u)) & 1u);
+    const bool hasFirst = leftFirst ? nd.hasL : nd.hasR, hasSecond = leftFirst ? nd.hasR : nd.hasL;
+    const bool takeFirst = hasFirst && !((cl >> fside) & 1u);
+    const bool takeSecond = hasSecond && !((cl >> (fside ^ 1u)) & 1u);
     const bool descend = !up && (takeFirst || takeSecond);
     const uint32_t nside = takeFirst ? fside : (fside ^ 1u);
     const bool lf = !up && !descend && nd.triSize > 0;
@@ -770,12 +787,12 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     if (COUNT && walk) cnt.aabb += (isRoot && curVis && !(fl & F_HITGEOM)) ? 0u : (stay ? 2u : 1u);
     // nodeIDs[ID] = true unless descending; nodeIDs[left] = nodeIDs[right] = true when climbing
     uint32_t ncb = cb | ((!descend && L > 0) ? (1u << vb) : 0u);
-    ncb |= climb ? ((left != -1 ? 1u : 0u) | (right != -1 ? 2u : 0u)) << ((2u * Lu) & 31u) : 0u;
+    ncb |= climb ? ((nd.hasL ? 1u : 0u) | (nd.hasR ? 2u : 0u)) << ((2u * Lu) & 31u) : 0u;
     const uint32_t dcb = (ncb & ~(3u << ((2u * Lu + 2u) & 31u))) | ((L == 0 && nside == 0u) ? (g << 2) : 0u);
     const bool runaway = guard >= S.trip_limit;
     uint32_t nfl = fl & ~(F_HITGEOM | F_LFIRST);
     nfl |= (!descend && L == 0) ? F_ROOTV : 0u;
-    nfl |= (climb && (left == -1 || right == -1)) ? F_SINK : 0u;
+    nfl |= (climb && !(nd.hasL && nd.hasR)) ? F_SINK : 0u;
     nfl |= hg ? F_HITGEOM : 0u;
     nfl |= ((isRoot && climb) || runaway) ? F_DONE : 0u;
     nfl |= runaway ? F_FAULT : 0u;
