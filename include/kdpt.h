@@ -255,7 +255,8 @@ int kdpt_count_split(kdpt_ctx *ctx, unsigned long long *aabb_prep_cand);
  * node-trip lanes waiting on a leaf, ... finished, cycles after the ray queue ran dry, finished
  * node-trip lanes then (each summed over waves), waves, wave cycles, aabb, tri, hit, then a 64-bin
  * histogram of intersect-wave lifetimes
- * (10 us bins) -- and returns how many exist. */
+ * (10 us bins), a 64-bin histogram of node steps per ray (bins of 4), and node steps summed / rays counted
+ * by the ray's chord through the KD root box (8 bins, eighths of its diagonal) -- and returns how many exist. */
 int kdpt_wave_profile(kdpt_ctx *ctx, unsigned long long *out, int n);
 /* Device-math known answers: sinf/cosf/pow-5 Fresnel/u01 evaluated by the gfx950 code. */
 int kdpt_selftest_math(const float *x, int n, float *sin_out, float *cos_out);

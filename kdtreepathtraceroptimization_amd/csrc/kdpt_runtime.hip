@@ -70,6 +70,9 @@ struct Counters {
   unsigned long long cand;       // rays handed to the intersect kernel
   unsigned long long wave[PROF_SLOTS + 2];  // WaveLeafLDS::prof summed over chunks, then chunks, cycles
   unsigned long long life[64];  // count mode: wave lifetimes in the intersect kernel, 10 us bins (s_memrealtime)
+  unsigned long long steps[64];  // count mode: node steps per ray, bins of 4
+  unsigned long long chord_steps[8], chord_n[8];  // ... summed by the ray's chord through the root box (8ths of
+                                                  // the box diagonal): does the chord predict a ray's cost?
 };
 
 __device__ inline unsigned int lane_prefix(unsigned long long mask) {
@@ -448,6 +451,22 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
     }
     // ---- finished rays: their hit record (what ShadeableIntersection would carry) ----
     if (pidx >= 0 && R.done) {
+      if (COUNT) {
+        const int st = R.guard;
+        atomicAdd(&A.counters->steps[min(st >> 2, 63)], 1ull);
+        const float4 lo = S.rlo, hi = S.rhi;
+        const float ax = (lo.x - R.o.x) * R.invdir.x, bx = (hi.x - R.o.x) * R.invdir.x;
+        const float ay = (lo.y - R.o.y) * R.invdir.y, by = (hi.y - R.o.y) * R.invdir.y;
+        const float az = (lo.z - R.o.z) * R.invdir.z, bz2 = (hi.z - R.o.z) * R.invdir.z;
+        const float t0 = fmaxf(fmaxf(fminf(ax, bx), fminf(ay, by)), fmaxf(fminf(az, bz2), 0.0f));
+        const float t1 = fminf(fminf(fmaxf(ax, bx), fmaxf(ay, by)), fmaxf(az, bz2));
+        const float dx = hi.x - lo.x, dy = hi.y - lo.y, dz = hi.z - lo.z;
+        const float diag = sqrtf(dx * dx + dy * dy + dz * dz);
+        const float f = diag > 0.0f ? 8.0f * fmaxf(t1 - t0, 0.0f) / diag : 0.0f;
+        const int cb = f >= 7.0f || !(f == f) ? 7 : (int)f;
+        atomicAdd(&A.counters->chord_steps[cb], (unsigned long long)st);
+        atomicAdd(&A.counters->chord_n[cb], 1ull);
+      }
       const Hit& h = R.h;
       const int code = h.hit_geom_index == -1 ? -1 : (h.obj_intersect ? -(R.objTri + 2) : h.hit_geom_index);
       int2* hits = pb == 0 ? A.it[0].hits : (pb == 1 ? A.it[1].hits : (pb == 2 ? A.it[2].hits : A.it[3].hits));
@@ -749,12 +768,12 @@ struct ShadeOut {
 };
 
 template <bool HYBRID, bool COMPACT>
-__device__ __attribute__((always_inline)) inline void shade_one(const ShadeArgs& A, const DevScene& S, int i, ShadeOut& o) {
+// hr = the path's hit record A.hits[i], loaded by the caller (k_shade_fused must read it before it lets later
+// tiles write the next bounce's records into the same array)
+__device__ __attribute__((always_inline)) inline void shade_one(const ShadeArgs& A, const DevScene& S, int i, int2 hr,
+                                                                ShadeOut& o) {
   const float4 q0 = A.paths.p0[i], q1 = A.paths.p1[i], q2 = A.paths.p2[i];
   int matHit = A.paths.pm[i];
-  // issued with the path loads (every listed slot has a record; unused when the path has no bounces
-  // left), not after the bounce test: one dependent HBM round trip less per path
-  const int2 hr = A.hits[i];
   const int pw = fbits(q1.w);
   const int pix = pw & 0x7fffffff;
   Ray ray;
@@ -865,7 +884,7 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   int key = 0;
   if (i < n) {
     ShadeOut o;
-    shade_one<HYBRID, COMPACT>(A, A.S, i, o);
+    shade_one<HYBRID, COMPACT>(A, A.S, i, A.hits[i], o);
     if (o.changed) {
       A.paths.p0[i] = o.q0;
       A.paths.p1[i] = o.q1;
@@ -928,12 +947,19 @@ __device__ inline unsigned long long lb_pack(unsigned long long flag, unsigned s
 }
 
 constexpr int STAGE_MATS = 32;
+#ifdef KDPT_SHADE_PROF  // tools/build_variant.sh experiments only: shading phase times (s_memrealtime ticks)
+__device__ unsigned long long g_shade_prof[8];
+#endif
+#ifndef KDPT_SHADE_TB
+#define KDPT_SHADE_TB 256  // tools/build_variant.sh experiments only
+#endif
+constexpr int SHADE_TB = KDPT_SHADE_TB;  // paths per fused-shading workgroup (one tile ticket each)
 
 // The LDS a shading workgroup uses: staged geoms/materials and the per-tile compaction scratch.
-template <bool STAGE>
+template <bool STAGE, int TB = TILE>
 struct ShadeLDS {
   int tile, b;
-  unsigned cnt[2][TILE / 64];
+  unsigned cnt[2][TB / 64];
   unsigned ex[2];
   uint32_t geoms[STAGE ? ORDERED_GEOMS * sizeof(DevGeom) / 4 : 1];
   uint32_t mats[STAGE ? STAGE_MATS * sizeof(DevMaterial) / 4 : 1];
@@ -941,14 +967,14 @@ struct ShadeLDS {
 
 // STAGE: the analytic geoms and the materials copied into LDS (small scenes: their per-lane reads, indexed
 // by hit and by nearest-first order, are then LDS reads instead of L2 round trips)
-template <bool STAGE>
-__device__ __attribute__((always_inline)) inline DevScene stage_scene(const DevScene& S0, ShadeLDS<STAGE>& L) {
+template <bool STAGE, int TB>
+__device__ __attribute__((always_inline)) inline DevScene stage_scene(const DevScene& S0, ShadeLDS<STAGE, TB>& L) {
   static_assert(sizeof(DevGeom) % 4 == 0 && sizeof(DevMaterial) % 4 == 0, "staged as dwords");
   DevScene S = S0;
   if (STAGE) {
     const int gw = S0.num_geoms * (int)(sizeof(DevGeom) / 4), mw = S0.num_materials * (int)(sizeof(DevMaterial) / 4);
-    for (int k = threadIdx.x; k < gw; k += TILE) L.geoms[k] = reinterpret_cast<const uint32_t*>(S0.geoms)[k];
-    for (int k = threadIdx.x; k < mw; k += TILE) L.mats[k] = reinterpret_cast<const uint32_t*>(S0.materials)[k];
+    for (int k = threadIdx.x; k < gw; k += TB) L.geoms[k] = reinterpret_cast<const uint32_t*>(S0.geoms)[k];
+    for (int k = threadIdx.x; k < mw; k += TB) L.mats[k] = reinterpret_cast<const uint32_t*>(S0.materials)[k];
     __syncthreads();
     S.geoms = reinterpret_cast<const DevGeom*>(L.geoms);
     S.materials = reinterpret_cast<const DevMaterial*>(L.mats);
@@ -956,37 +982,69 @@ __device__ __attribute__((always_inline)) inline DevScene stage_scene(const DevS
   return S;
 }
 
+// shade()'s outcome for path i ahead of the shading: bounces left after this bounce != 0.  A listed hit
+// has t > 0 (the traversal and k_geoms/prep_ray keep only t > 0, and shade_one recomputes the same t), so
+// the path survives iff it has bounces left, hit something, the hit material does not emit, and one bounce
+// remains after this one.
+__device__ __attribute__((always_inline)) inline bool survives(const ShadeArgs& A, const DevScene& S, int i, int2 hr) {
+  const int bounces = fbits(A.paths.p2[i].w);
+  if (bounces <= 0) return bounces != 0;
+  if (hr.x == -1) return false;
+  const int mid = hr.x < -1 ? hr.y : S.geoms[hr.x].materialid;
+  return !(S.materials[mid].emittance > 0.0f) && bounces - 1 != 0;
+}
+
 // One 256-path tile of one iteration: shading, the survivors' stable compaction into the other path buffer
 // (decoupled look-back over the earlier tiles' records), the next bounce's intersect-stage hand-off.  Tiles
 // of an iteration must be started in increasing order (tickets), so every earlier tile is already running.
-template <bool HYBRID, bool STAGE>
+template <bool HYBRID, bool STAGE, int TB>
 __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs& A, const FuseArgs& F, const DevScene& S, int tile, int n,
-                                  ShadeLDS<STAGE>& L) {
-  const int i = tile * TILE + threadIdx.x;
+                                  ShadeLDS<STAGE, TB>& L) {
+  const int i = tile * TB + threadIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+#ifdef KDPT_SHADE_PROF
+  const unsigned long long pt0 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (i == 0) shade_stats(A, n);
-  ShadeOut o;
-  o.alive = o.walk = o.tested = false;
-  if (i < n) shade_one<HYBRID, true>(A, S, i, o);
-  const unsigned long long ms = __ballot(o.alive), mw = __ballot(o.walk);
-  if (A.count_aabb && A.prep_on) count_prep(A, o.tested, o.walk);
-  if (lane == 0) {
-    L.cnt[0][wid] = (unsigned)__popcll(ms);
-    L.cnt[1][wid] = (unsigned)__popcll(mw);
-  }
+  unsigned long long* lb = F.lb + (size_t)A.depth * A.ntiles;
+  // (1) Which paths survive this bounce follows from the hit record and the hit material alone, so the
+  // tile's survivor count is published (look-back aggregate) before the shading: later tiles' look-backs
+  // then wait on this tile's two loads, not on its whole shading (measured: the look-back wait had grown
+  // as long as the shading itself, the slowest of 64 predecessors' shading each time).
+  // the hit record is read once, here: once this tile's aggregate is out, later tiles may finish their
+  // look-back and write the next bounce's records (F.hits == A.hits) into this tile's index range
+  const int2 hr = i < n ? A.hits[i] : make_int2(-1, -1);
+  const bool pred = i < n && survives(A, S, i, hr);
+  const unsigned long long ms = __ballot(pred);
+  if (lane == 0) L.cnt[0][wid] = (unsigned)__popcll(ms);
   __syncthreads();
   if (wid == 0) {
+    unsigned aS = 0;
+    for (int w = 0; w < TB / 64; w++) aS += L.cnt[0][w];
+    if (lane == 0) lb_store(lb + tile, lb_pack(tile == 0 ? 2 : 1, aS, 0));
+  }
+  // (2) the shading
+  ShadeOut o;
+  o.alive = o.walk = o.tested = false;
+  if (i < n) shade_one<HYBRID, true>(A, S, i, hr, o);
+  if (o.alive != pred) atomicOr(S.fault, 32);  // unreachable: survives() restates shade()'s outcome
+  const unsigned long long mw = __ballot(o.walk);
+  if (A.count_aabb && A.prep_on) count_prep(A, o.tested, o.walk);
+  if (lane == 0) L.cnt[1][wid] = (unsigned)__popcll(mw);
+  __syncthreads();
+#ifdef KDPT_SHADE_PROF
+  const unsigned long long pt1 = __builtin_amdgcn_s_memrealtime();
+#endif
+  // (3) the survivors' exclusive prefix (look-back), the walkers' place in the next bounce's candidate
+  // list (one counter add per tile: the list's order only decides which lane traces which ray)
+  if (wid == 0) {
     unsigned aS = 0, aW = 0;
-    for (int w = 0; w < TILE / 64; w++) {
+    for (int w = 0; w < TB / 64; w++) {
       aS += L.cnt[0][w];
       aW += L.cnt[1][w];
     }
-    unsigned long long* lb = F.lb + (size_t)A.depth * A.ntiles;
-    unsigned eS = 0, eW = 0;
-    if (tile == 0) {
-      if (lane == 0) lb_store(lb, lb_pack(2, aS, aW));
-    } else {
-      if (lane == 0) lb_store(lb + tile, lb_pack(1, aS, aW));
+    unsigned eS = 0;
+    if (tile != 0) {
       for (int base = tile - 1;; base -= 64) {
         const int j = base - lane;
         unsigned long long v = j >= 0 ? lb_load(lb + j) : lb_pack(2, 0, 0);
@@ -996,28 +1054,23 @@ __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs
         }
         const unsigned long long pre = __ballot((v >> 62) == 2);
         const int upto = pre ? __ffsll((long long)pre) - 1 : 63;  // nearest inclusive prefix, and the counts before it
-        unsigned s = lane <= upto ? (unsigned)(v >> 31) & 0x7fffffffu : 0u;
-        unsigned w = lane <= upto ? (unsigned)v & 0x7fffffffu : 0u;
-        for (int off = 32; off > 0; off >>= 1) {
-          s += __shfl_xor(s, off);
-          w += __shfl_xor(w, off);
-        }
-        eS += s;
-        eW += w;
+        unsigned sm = lane <= upto ? (unsigned)(v >> 31) & 0x7fffffffu : 0u;
+        for (int off = 32; off > 0; off >>= 1) sm += __shfl_xor(sm, off);
+        eS += sm;
         if (pre) break;
       }
-      if (lane == 0) lb_store(lb + tile, lb_pack(2, eS + aS, eW + aW));
+      if (lane == 0) lb_store(lb + tile, lb_pack(2, eS + aS, 0));
     }
     if (lane == 0) {
       L.ex[0] = eS;
-      L.ex[1] = eW;
-      if (tile == (n - 1) / TILE) {  // the last tile: the next bounce's path and candidate counts
-        F.counts[A.depth + 1] = (int)(eS + aS);
-        if (A.prep_on) F.ccount[A.depth + 1] = (int)(eW + aW);
-      }
+      L.ex[1] = (A.prep_on && aW) ? (unsigned)atomicAdd(&F.ccount[A.depth + 1], (int)aW) : 0u;
+      if (tile == (n - 1) / TB) F.counts[A.depth + 1] = (int)(eS + aS);  // the last tile: the next bounce's paths
     }
   }
   __syncthreads();
+#ifdef KDPT_SHADE_PROF
+  const unsigned long long pt2 = __builtin_amdgcn_s_memrealtime();
+#endif
   if (o.alive) {
     unsigned bS = L.ex[0], bW = L.ex[1];
     for (int w = 0; w < wid; w++) {
@@ -1038,21 +1091,32 @@ __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs
       }
     }
   }
+#ifdef KDPT_SHADE_PROF
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned long long pt3 = __builtin_amdgcn_s_memrealtime();
+    atomicAdd(&g_shade_prof[0], pt1 - pt0);
+    atomicAdd(&g_shade_prof[1], pt2 - pt1);
+    atomicAdd(&g_shade_prof[2], pt3 - pt2);
+    atomicAdd(&g_shade_prof[3], 1ull);
+    atomicAdd(&g_shade_prof[4], (unsigned long long)min(TB, n - tile * TB));
+  }
+#endif
 }
 
 // One launch per bounce and iteration: tile = ticket (tickets start the tiles in order).
 template <bool HYBRID, bool STAGE>
-__global__ __launch_bounds__(TILE) void k_shade_fused(ShadeArgs A, FuseArgs F) {
+__global__ __launch_bounds__(SHADE_TB) void k_shade_fused(ShadeArgs A, FuseArgs F) {
   const int n = A.counts[A.depth];
   // the grid covers every pixel, so past the first bounces most workgroups have no tile: exactly the first
-  // ceil(n / TILE) take tickets (one contended atomic per tile, not per workgroup), the rest leave at once
-  if ((int)blockIdx.x * TILE >= n) return;
-  __shared__ ShadeLDS<STAGE> L;
+  // ceil(n / SHADE_TB) take tickets (one contended atomic per tile, not per workgroup), the rest leave at once
+  if ((int)blockIdx.x * SHADE_TB >= n) return;
+  __shared__ ShadeLDS<STAGE, SHADE_TB> L;
   if (threadIdx.x == 0) L.tile = atomicAdd(&F.tickets[A.depth], 1);
   __syncthreads();
   const int tile = L.tile;
-  const DevScene S = stage_scene<STAGE>(A.S, L);
-  shade_tile<HYBRID, STAGE>(A, F, S, tile, n, L);
+  const DevScene S = stage_scene<STAGE, SHADE_TB>(A.S, L);
+  shade_tile<HYBRID, STAGE, SHADE_TB>(A, F, S, tile, n, L);
 }
 
 // Exclusive scan of the tile counts (one workgroup; <= MAX_KEYS * ntiles entries).
@@ -1719,6 +1783,9 @@ int setup_trace(kdpt_ctx* c) {
 // the iteration then reports an error instead of returning a silently wrong image.
 int fault_error(kdpt_ctx* c, int code) {
   (void)hipMemset(c->counts + c->cap + 2, 0, sizeof(int));
+  if (code & 32)
+    return fail(KDPT_ERR_HIP, "shading: a path's survival differed from its hit record's prediction, code " +
+                                  std::to_string(code));
   return fail(KDPT_ERR_HIP, "KD traversal exceeded its step bound (inconsistent tree), code " + std::to_string(code));
 }
 
@@ -1730,6 +1797,14 @@ int check_fault(kdpt_ctx* c) {
 
 }  // namespace
 
+#ifdef KDPT_SHADE_PROF
+extern "C" int kdpt_debug_shade_prof(unsigned long long* out) {  // sums, then zeroes, the counters
+  const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_shade_prof), sizeof(zero)) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_shade_prof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 extern "C" {
 
 void kdpt_default_options(kdpt_options* o) {
@@ -2515,7 +2590,10 @@ int kdpt_wave_profile(kdpt_ctx* c, unsigned long long* out, int n) {
   int k = 0;
   for (; k < n && k < PROF_SLOTS + 5; k++) out[k] = v[k];
   for (int b = 0; b < 64 && k < n; b++, k++) out[k] = c->last_profile.life[b];
-  return PROF_SLOTS + 5 + 64;
+  for (int b = 0; b < 64 && k < n; b++, k++) out[k] = c->last_profile.steps[b];
+  for (int b = 0; b < 8 && k < n; b++, k++) out[k] = c->last_profile.chord_steps[b];
+  for (int b = 0; b < 8 && k < n; b++, k++) out[k] = c->last_profile.chord_n[b];
+  return PROF_SLOTS + 5 + 64 + 64 + 16;
 }
 
 int kdpt_selftest_math(const float* x, int n, float* so, float* co) {
@@ -2764,10 +2842,11 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         const FuseArgs f{c->buf[nxt], c->tickets, c->lb, c->counts, c->ccount, c->geomhit, c->hits, c->cand};
         const bool stage = c->S.num_geoms + c->S.num_boxes <= ORDERED_GEOMS && c->S.num_materials <= STAGE_MATS;
         const bool hyb = c->opt.short_stack || c->brute;
-        if (hyb && stage) hipLaunchKernelGGL((k_shade_fused<true, true>), dim3(c->ntiles), dim3(TILE), 0, st, a, f);
-        else if (hyb) hipLaunchKernelGGL((k_shade_fused<true, false>), dim3(c->ntiles), dim3(TILE), 0, st, a, f);
-        else if (stage) hipLaunchKernelGGL((k_shade_fused<false, true>), dim3(c->ntiles), dim3(TILE), 0, st, a, f);
-        else hipLaunchKernelGGL((k_shade_fused<false, false>), dim3(c->ntiles), dim3(TILE), 0, st, a, f);
+        const int shade_grid = (c->npix + SHADE_TB - 1) / SHADE_TB;
+        if (hyb && stage) hipLaunchKernelGGL((k_shade_fused<true, true>), dim3(shade_grid), dim3(SHADE_TB), 0, st, a, f);
+        else if (hyb) hipLaunchKernelGGL((k_shade_fused<true, false>), dim3(shade_grid), dim3(SHADE_TB), 0, st, a, f);
+        else if (stage) hipLaunchKernelGGL((k_shade_fused<false, true>), dim3(shade_grid), dim3(SHADE_TB), 0, st, a, f);
+        else hipLaunchKernelGGL((k_shade_fused<false, false>), dim3(shade_grid), dim3(SHADE_TB), 0, st, a, f);
         HIP_TRY(hipGetLastError());
         c->cur = nxt;
         continue;
