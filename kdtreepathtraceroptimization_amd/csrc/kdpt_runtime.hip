@@ -767,13 +767,47 @@ struct ShadeOut {
   int gh;
 };
 
+// Everything one path's shading reads from memory, loaded in one go: the path, its hit record, the pixel's
+// accumulated value (COMPACT: partialGather) and the hit triangle's vertex, edge and normal records (all in
+// flight together; k_shade_fused issues them before its publication barrier, and must read the hit record
+// before it lets later tiles write the next bounce's records into the same array).
+struct ShadeIn {
+  float4 q0, q1, q2;
+  int pm;
+  int2 hr;
+  float3 px_old;
+  TriData T;
+  float4 n1v, n2v, n3v;
+};
+
+template <bool COMPACT>
+__device__ __attribute__((always_inline)) inline void shade_load(const ShadeArgs& A, const DevScene& S, int i,
+                                                                 ShadeIn& in) {
+  in.q0 = A.paths.p0[i];
+  in.q1 = A.paths.p1[i];
+  in.q2 = A.paths.p2[i];
+  in.pm = A.paths.pm[i];
+  in.hr = A.hits[i];
+  in.px_old = make_float3(0.0f, 0.0f, 0.0f);
+  if (COMPACT) {
+    const float* px = A.image + 3 * (size_t)(fbits(in.q1.w) & 0x7fffffff);
+    in.px_old = make_float3(px[0], px[1], px[2]);
+  }
+  if (in.hr.x < -1 && fbits(in.q2.w) > 0) {
+    const int k = -in.hr.x - 2;
+    in.T = TriData{S.tv0[k], S.te1[k], S.te2[k]};
+    in.n1v = S.tn0[k];
+    in.n2v = S.tn1[k];
+    in.n3v = S.tn2[k];
+  }
+}
+
 template <bool HYBRID, bool COMPACT>
-// hr = the path's hit record A.hits[i], loaded by the caller (k_shade_fused must read it before it lets later
-// tiles write the next bounce's records into the same array)
-__device__ __attribute__((always_inline)) inline void shade_one(const ShadeArgs& A, const DevScene& S, int i, int2 hr,
-                                                                ShadeOut& o) {
-  const float4 q0 = A.paths.p0[i], q1 = A.paths.p1[i], q2 = A.paths.p2[i];
-  int matHit = A.paths.pm[i];
+__device__ __attribute__((always_inline)) inline void shade_one(const ShadeArgs& A, const DevScene& S, int i,
+                                                                const ShadeIn& in, ShadeOut& o) {
+  const float4 q0 = in.q0, q1 = in.q1, q2 = in.q2;
+  int matHit = in.pm;
+  const int2 hr = in.hr;
   const int pw = fbits(q1.w);
   const int pix = pw & 0x7fffffff;
   Ray ray;
@@ -784,13 +818,7 @@ __device__ __attribute__((always_inline)) inline void shade_one(const ShadeArgs&
   f3 color = mk3(q2.x, q2.y, q2.z);
   int bounces = fbits(q2.w);
   o.changed = bounces > 0;
-  // the pixel's accumulated value (partialGather below), fetched with the hit's triangle instead of after
-  // the shading: one dependent HBM round trip less for the paths that end at this bounce
-  float3 px_old = make_float3(0.0f, 0.0f, 0.0f);
-  if (COMPACT) {
-    const float* px = A.image + 3 * (size_t)pix;
-    px_old = make_float3(px[0], px[1], px[2]);
-  }
+  const float3 px_old = in.px_old;
   if (bounces > 0) {
     float isect_t = -1.0f;
     int isect_mat = 0;
@@ -799,13 +827,9 @@ __device__ __attribute__((always_inline)) inline void shade_one(const ShadeArgs&
       float t;
       int mid;
       if (hr.x < -1) {  // triangle: the traversal's final recomputation, repeated
-        const int k = -hr.x - 2;
-        // all six records in flight at once (vertex, edges, normals), then the arithmetic
-        const TriData T{S.tv0[k], S.te1[k], S.te2[k]};
-        const float4 n1v = S.tn0[k], n2v = S.tn1[k], n3v = S.tn2[k];
         float bx, by, bzk;
-        tri_test_v(T, ray.origin, ray.direction, bx, by, bzk);
-        t = tri_hit_t_n<HYBRID>(n1v, n2v, n3v, ray.origin, ray.direction, bx, by, bzk, ip, nrm);
+        tri_test_v(in.T, ray.origin, ray.direction, bx, by, bzk);
+        t = tri_hit_t_n<HYBRID>(in.n1v, in.n2v, in.n3v, ray.origin, ray.direction, bx, by, bzk, ip, nrm);
         mid = hr.y;
       } else {
         const DevGeom& G = S.geoms[hr.x];
@@ -884,7 +908,9 @@ __global__ __launch_bounds__(TILE) void k_shade(ShadeArgs A) {
   int key = 0;
   if (i < n) {
     ShadeOut o;
-    shade_one<HYBRID, COMPACT>(A, A.S, i, A.hits[i], o);
+    ShadeIn in;
+    shade_load<COMPACT>(A, A.S, i, in);
+    shade_one<HYBRID, COMPACT>(A, A.S, i, in, o);
     if (o.changed) {
       A.paths.p0[i] = o.q0;
       A.paths.p1[i] = o.q1;
@@ -986,8 +1012,7 @@ __device__ __attribute__((always_inline)) inline DevScene stage_scene(const DevS
 // has t > 0 (the traversal and k_geoms/prep_ray keep only t > 0, and shade_one recomputes the same t), so
 // the path survives iff it has bounces left, hit something, the hit material does not emit, and one bounce
 // remains after this one.
-__device__ __attribute__((always_inline)) inline bool survives(const ShadeArgs& A, const DevScene& S, int i, int2 hr) {
-  const int bounces = fbits(A.paths.p2[i].w);
+__device__ __attribute__((always_inline)) inline bool survives(const DevScene& S, int bounces, int2 hr) {
   if (bounces <= 0) return bounces != 0;
   if (hr.x == -1) return false;
   const int mid = hr.x < -1 ? hr.y : S.geoms[hr.x].materialid;
@@ -1013,8 +1038,10 @@ __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs
   // as long as the shading itself, the slowest of 64 predecessors' shading each time).
   // the hit record is read once, here: once this tile's aggregate is out, later tiles may finish their
   // look-back and write the next bounce's records (F.hits == A.hits) into this tile's index range
-  const int2 hr = i < n ? A.hits[i] : make_int2(-1, -1);
-  const bool pred = i < n && survives(A, S, i, hr);
+  ShadeIn in;
+  in.hr = make_int2(-1, -1);
+  if (i < n) shade_load<true>(A, S, i, in);
+  const bool pred = i < n && survives(S, fbits(in.q2.w), in.hr);
   const unsigned long long ms = __ballot(pred);
   if (lane == 0) L.cnt[0][wid] = (unsigned)__popcll(ms);
   __syncthreads();
@@ -1026,7 +1053,7 @@ __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs
   // (2) the shading
   ShadeOut o;
   o.alive = o.walk = o.tested = false;
-  if (i < n) shade_one<HYBRID, true>(A, S, i, hr, o);
+  if (i < n) shade_one<HYBRID, true>(A, S, i, in, o);
   if (o.alive != pred) atomicOr(S.fault, 32);  // unreachable: survives() restates shade()'s outcome
   const unsigned long long mw = __ballot(o.walk);
   if (A.count_aabb && A.prep_on) count_prep(A, o.tested, o.walk);
