@@ -478,8 +478,8 @@ class PathTracer:
 
     def wave_profile(self):
         """Cycle profile of the intersect kernel in the last count_iteration (kdpt_wave_profile)."""
-        out = (C.c_ulonglong * 128)()
-        n = self.lib.kdpt_wave_profile(self._ctx, out, 128)
+        out = (C.c_ulonglong * 256)()
+        n = self.lib.kdpt_wave_profile(self._ctx, out, 256)
         _check(0 if n > 0 else n, "kdpt_wave_profile")
         keys = ("node_trips", "node_cycles", "big_sweeps", "big_cycles", "small_phases", "small_rounds",
                 "small_cycles", "final_cycles", "setup_cycles", "geom_cycles", "post_cycles", "node_lane_steps",
@@ -487,8 +487,13 @@ class PathTracer:
                 "node_done_steps", "tail_cycles", "tail_node_done_steps",
                 "chunks", "chunk_cycles", "aabb", "tri", "hit")
         prof = dict(zip(keys, (int(out[k]) for k in range(len(keys)))))
-        if n > len(keys):
-            prof["wave_life_10us"] = [int(out[k]) for k in range(len(keys), min(n, 128))]
+        k0 = len(keys)
+        if n >= k0 + 64:
+            prof["wave_life_10us"] = [int(out[k]) for k in range(k0, k0 + 64)]
+        if n >= k0 + 144:
+            prof["ray_steps_hist4"] = [int(out[k]) for k in range(k0 + 64, k0 + 128)]
+            prof["chord_steps"] = [int(out[k]) for k in range(k0 + 128, k0 + 136)]
+            prof["chord_rays"] = [int(out[k]) for k in range(k0 + 136, k0 + 144)]
         return prof
 
     def close(self):

@@ -19,6 +19,12 @@ for cfg in (sys.argv[2] if len(sys.argv) > 2 else "1x1,2x2,1x4").split(","):
     pt.synchronize()
     prof = pt.wave_profile()
     prof.pop("wave_life_10us", None)
+    hist = prof.pop("ray_steps_hist4", None)
+    cs, cn = prof.pop("chord_steps", None), prof.pop("chord_rays", None)
+    if hist:
+        print(json.dumps({"cfg": cfg, "ray_steps_hist4": hist,
+                          "steps_by_chord8": [round(a / max(1, b), 1) for a, b in zip(cs, cn)], "rays_by_chord8": cn}),
+              flush=True)
     rays = max(1, pt.stats().total_trace_rays)
     print(json.dumps({"cfg": cfg, "rays": rays, "per_ray": {k: round(v / rays, 3) for k, v in prof.items()}}),
           flush=True)
