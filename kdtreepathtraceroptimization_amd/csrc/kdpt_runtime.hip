@@ -1133,7 +1133,7 @@ __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs
 
 // One launch per bounce and iteration: tile = ticket (tickets start the tiles in order).
 template <bool HYBRID, bool STAGE>
-__global__ __launch_bounds__(SHADE_TB) void k_shade_fused(ShadeArgs A, FuseArgs F) {
+__global__ __launch_bounds__(SHADE_TB) __attribute__((amdgpu_waves_per_eu(6))) void k_shade_fused(ShadeArgs A, FuseArgs F) {
   const int n = A.counts[A.depth];
   // the grid covers every pixel, so past the first bounces most workgroups have no tile: exactly the first
   // ceil(n / SHADE_TB) take tickets (one contended atomic per tile, not per workgroup), the rest leave at once
