@@ -470,7 +470,9 @@ struct NodesPacked {
   static constexpr bool kLeafHoldsCluster = true;  // big leaves: triStart holds the first cluster
   const int4* p;  // global or LDS (address space inferred after inlining)
   __device__ NodeRec operator()(int i) const {
-    const int4 q0 = p[2 * i], q1 = p[2 * i + 1];
+    // two 16-byte vector loads (as int4 fields the compiler reads the record in four pieces)
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const v4i q0 = reinterpret_cast<const v4i*>(p)[2 * i], q1 = reinterpret_cast<const v4i*>(p)[2 * i + 1];
     NodeRec r;
     r.b0 = make_float4(ibits(q0.x), ibits(q0.y), ibits(q0.z), ibits(q0.w));
     r.b1 = make_float4(ibits(q1.x), ibits(q1.y), 0.0f, 0.0f);
@@ -647,6 +649,7 @@ __device__ inline int pair_owner(int* slot, int excl, int cnt, int B, int& carry
 
 __device__ inline TriData tri_load(const DevScene& S, int i) { return TriData{S.tv0[i], S.te1[i], S.te2[i]}; }
 
+
 __device__ inline int tri_test(const DevScene& S, int i, f3 o, f3 d, float& bx, float& by, float& bz) {
   return tri_test_v(tri_load(S, i), o, d, bx, by, bz);
 }
@@ -730,7 +733,6 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   int& objTri = R.objTri;
   // ---------------- node phase ----------------
   bool leaf = false;
-  int lstart = 0, lsize = 0, lparent = -1, lnode = 0;
   bool lfirst = true;
   int trips = 0;
   if (COUNT) prof_lap(W, -1);
@@ -805,10 +807,6 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       L += descend ? 1 : (climb ? -1 : 0);
       guard++;
       fl = nfl;
-      lstart = nd.triStart;
-      lsize = nd.triSize;
-      lparent = nd.parent;
-      lnode = cur;
     }
   }
   rootv = (fl & F_ROOTV) != 0u;
@@ -825,6 +823,16 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   }
   if (__any(fault) && lane == 0) atomicOr(S.fault, 1);
   if (!__any(leaf)) return;
+  // the leaf's own record, read once here rather than carried through every node trip (a lane that reaches
+  // a leaf neither climbs nor descends, so cur is the leaf)
+  const int lnode = cur;
+  int lstart = 0, lsize = 0, lparent = -1;
+  if (leaf) {
+    const NodeRec ln = nodes(cur);
+    lstart = ln.triStart;
+    lsize = ln.triSize;
+    lparent = ln.parent;
+  }
   // ---------------- leaf phase (wave-cooperative) ----------------
   // per lane results of this phase
   int r_pass = 0;          // 0 = none, else tri + 1 of the last u/v pass
