@@ -173,7 +173,10 @@ constexpr int trace_block() { return MODE == 2 ? TRACE_BLOCK : 256; }
 
 // Up to MAXB iterations (each its own path buffers) at the same bounce share one intersect launch:
 // more rays per launch keep the lanes of the persistent waves busy.
-constexpr int MAXB = 4;
+#ifndef KDPT_MAXB
+#define KDPT_MAXB 4  // tools/build_variant.sh experiments only
+#endif
+constexpr int MAXB = KDPT_MAXB;
 struct TraceIter {
   PathBuf paths;
   const int* cand;      // k_geoms' list of the paths whose ray meets the KD root box (queue slot -> path)
@@ -422,12 +425,25 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
       }
       if (COUNT && exhausted && lane == 0 && !W->tail_t0) W->tail_t0 = __builtin_readcyclecounter();
       if (pidx < 0 && k < n) {
-        const int b = (k >= pre[1]) + (k >= pre[2]) + (k >= pre[3]);
-        const TraceIter& I = b == 0 ? A.it[0] : (b == 1 ? A.it[1] : (b == 2 ? A.it[2] : A.it[3]));
-        const int local = k - (b == 0 ? 0 : (b == 1 ? pre[1] : (b == 2 ? pre[2] : pre[3])));
-        const int i = I.cand[local];
-        const float4 q0 = I.paths.p0[i], q1 = I.paths.p1[i];
-        const int2 gh = I.geomhit[i];
+        int b = 0;
+#pragma unroll
+        for (int q = 1; q < MAXB; q++) b += k >= pre[q];
+        const int* cand = A.it[0].cand;
+        const float4 *p0 = A.it[0].paths.p0, *p1 = A.it[0].paths.p1;
+        const int2* ghp = A.it[0].geomhit;
+        int local = k;
+#pragma unroll
+        for (int q = 1; q < MAXB; q++)
+          if (b == q) {
+            cand = A.it[q].cand;
+            p0 = A.it[q].paths.p0;
+            p1 = A.it[q].paths.p1;
+            ghp = A.it[q].geomhit;
+            local = k - pre[q];
+          }
+        const int i = cand[local];
+        const float4 q0 = p0[i], q1 = p1[i];
+        const int2 gh = ghp[i];
         pidx = i;
         pb = b;
         wave_ray_start(S, R, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z), u2f((uint32_t)gh.x), gh.y, W);
@@ -469,7 +485,10 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
       }
       const Hit& h = R.h;
       const int code = h.hit_geom_index == -1 ? -1 : (h.obj_intersect ? -(R.objTri + 2) : h.hit_geom_index);
-      int2* hits = pb == 0 ? A.it[0].hits : (pb == 1 ? A.it[1].hits : (pb == 2 ? A.it[2].hits : A.it[3].hits));
+      int2* hits = A.it[0].hits;
+#pragma unroll
+      for (int q = 1; q < MAXB; q++)
+        if (pb == q) hits = A.it[q].hits;
       hits[pidx] = make_int2(code, h.objMaterialIdx);
       pidx = -1;
     }
