@@ -419,7 +419,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
       } else {
         int b = 0;
         if (lane == 0) b = nwaves * srun + atomicAdd(work, __popcll(im));
-        const int base = __shfl(b, 0);
+        const int base = __builtin_amdgcn_readfirstlane(b);  // lane 0 is active: the whole wave is here
         k = base + p;
         exhausted = base + __popcll(im) >= n;  // the counter only grows: later rounds find nothing
       }
