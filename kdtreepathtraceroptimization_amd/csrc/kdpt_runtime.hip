@@ -2183,10 +2183,11 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   // The product reads no environment variables: every route is the tested default unless a caller
   // changes it explicitly with kdpt_set_tuning (A/B experiments, the three-kernel compaction test).
   c->S.trace_mode = 0;
-  // leave the node phase early once at most 32 lanes still walk and at least 24 wait on a leaf (the
-  // walkers resume after the leaf phase; A/B over the bench: 3 390 -> 3 540 Mrays/s; 0 / 65 = never)
-  c->S.early_walk = 32;
-  c->S.early_leaf = 24;
+  // leave the node phase early once at most early_walk lanes still walk and at least early_leaf wait on a
+  // leaf (the walkers resume after the leaf phase; first A/B at 32 / 24: 3 390 -> 3 540 Mrays/s; 0 / 65 =
+  // never)
+  c->S.early_walk = 24;  // re-swept after the flattened leaf phase made leaf phases cheaper (32 / 24 before):
+  c->S.early_leaf = 1;   // 4 505-4 530 -> 4 659-4 704 Mrays/s, k_trace launch 0.85 -> 0.80 ms
   c->trace_order = false;  // superseded by k_geoms' candidate lists
   if ((rc = setup_trace(c))) return bail(rc);
   c->S.trip_limit = 8 * std::max(c->S.num_nodes, 1) + 64;
