@@ -537,7 +537,10 @@ __device__ inline void prof_lap(WaveLeafLDS* W, int k) {  // cycles since the la
   }
 }
 
-constexpr int BIG_LEAF = 64;  // leaves this size or larger are swept by the whole wave, one at a time
+#ifndef KDPT_BIG_LEAF
+#define KDPT_BIG_LEAF 64  // tools/build_variant.sh experiments only
+#endif
+constexpr int BIG_LEAF = KDPT_BIG_LEAF;  // leaves this size or larger are tested cluster by cluster
 
 __device__ inline float readlane_f(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
