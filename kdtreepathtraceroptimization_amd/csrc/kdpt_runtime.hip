@@ -189,6 +189,7 @@ struct TraceArgs {
   DevScene S;
   TraceIter it[MAXB];
   int nb;
+  int prof_steps;  // count mode, "profile_batches" = 2: per-ray node-step histogram
   int* work;  // chunk counters, zeroed by k_gen_rays (of iteration 0 of the batch)
   int depth;
   Counters* counters;
@@ -467,7 +468,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
     }
     // ---- finished rays: their hit record (what ShadeableIntersection would carry) ----
     if (pidx >= 0 && R.done) {
-      if (COUNT) {
+      if (COUNT && A.prof_steps) {  // (its atomics distort the cycle profile: a separate run)
         const int st = R.guard;
         atomicAdd(&A.counters->steps[min(st >> 2, 63)], 1ull);
         const float4 lo = S.rlo, hi = S.rhi;
@@ -1481,6 +1482,7 @@ struct kdpt_ctx {
   std::vector<kdpt_ctx*> slots;
   int slot_batch = 1;
   bool profile_batches = false;
+  bool profile_steps = false;  // "profile_batches" = 2
   std::vector<hipEvent_t> slot_done, slot_free;
   hipStream_t accum_stream = nullptr;
   hipEvent_t accum_ev = nullptr;  // recorded on accum_stream; c->stream waits on it (join_accum)
@@ -2266,6 +2268,7 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     if (c->grid_env) c->trace_grid = std::max(1, (int)(c->full_trace_grid * frac));
   } else if (k == "profile_batches") {
     c->profile_batches = v != 0;
+    c->profile_steps = v >= 2;
   } else if (k == "sync_debug") {
     c->sync_debug = v != 0;
   } else {
@@ -2784,6 +2787,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     TraceArgs t;
     t.S = c0->S;
     t.nb = nb;
+    t.prof_steps = (c0->parent ? c0->parent : c0)->profile_steps ? 1 : 0;
     for (int b = 0; b < MAXB; b++) {
       kdpt_ctx* c = cs[b < nb ? b : 0];
       t.it[b].paths = c->buf[c->cur];
