@@ -345,6 +345,10 @@ __global__ __launch_bounds__(GEOM_BLOCK) void k_geoms(DevScene S, PathBuf paths,
   if (threadIdx.x == 0) atomicMax(&gspan[2 * depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
+#ifdef KDPT_TAIL_PROF  // tools/build_variant.sh experiments only: intersect workgroup life / tail (ticks)
+__device__ unsigned long long g_tail_prof[4];
+#endif
+
 // KD traversal of every live path.  Each lane holds one ray; whenever rays finish, the idle lanes take
 // the next paths of the bounce from a device counter, so a wave stays full until the bounce runs out
 // of paths (the per-ray algorithm is unchanged -- only which lane runs it, and when).
@@ -378,9 +382,16 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
   // launch duration on the device clock (first block start .. last block end); the HIP events around
   // the launch also count time spent queued behind other streams' kernels when iterations overlap
   __shared__ int s_waves_done;
+#ifdef KDPT_TAIL_PROF
+  __shared__ unsigned long long s_t0, s_tex;
+#endif
   if (threadIdx.x == 0) {
     s_waves_done = 0;
     atomicMin(&A.trace_t[2 * A.depth], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#ifdef KDPT_TAIL_PROF
+    s_t0 = __builtin_amdgcn_s_memrealtime();
+    s_tex = ~0ull;
+#endif
   }
   __syncthreads();
   int* work = A.work + A.depth;
@@ -402,6 +413,9 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
   const int srun = KDPT_SRUN_SPREAD ? min(64, max(1, (n + nwaves - 1) / nwaves)) : 64;
   bool first = true, exhausted = false;
   long long rounds = 0;
+#ifdef KDPT_TAIL_PROF
+  unsigned long long tex_seen = 0;
+#endif
   while (true) {
     if (__ballot(1) != ~0ull) {  // the refill protocol needs the whole wave here
       atomicOr(S.fault, 4);
@@ -425,6 +439,9 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
         exhausted = base + __popcll(im) >= n;  // the counter only grows: later rounds find nothing
       }
       if (COUNT && exhausted && lane == 0 && !W->tail_t0) W->tail_t0 = __builtin_readcyclecounter();
+#ifdef KDPT_TAIL_PROF
+      if (exhausted && !tex_seen) tex_seen = __builtin_amdgcn_s_memrealtime();
+#endif
       if (pidx < 0 && k < n) {
         int b = 0;
 #pragma unroll
@@ -508,8 +525,20 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
       atomicAdd(&A.counters->life[us10 < 63 ? us10 : 63], 1ull);
     }
   }
-  if (lane == 0 && atomicAdd(&s_waves_done, 1) == TB / 64 - 1)
+#ifdef KDPT_TAIL_PROF
+  if (lane == 0 && tex_seen) atomicMin(&s_tex, tex_seen);
+#endif
+  if (lane == 0 && atomicAdd(&s_waves_done, 1) == TB / 64 - 1) {
     atomicMax(&A.trace_t[2 * A.depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+#ifdef KDPT_TAIL_PROF
+    // this workgroup's life, and its part after its first wave found the ray queue empty
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long tex = s_tex == ~0ull ? t1 : s_tex;
+    atomicAdd(&g_tail_prof[0], t1 - s_t0);
+    atomicAdd(&g_tail_prof[1], t1 - (tex < s_t0 ? s_t0 : tex));
+    atomicAdd(&g_tail_prof[2], 1ull);
+#endif
+  }
 }
 
 // ---------------------------------------------------------------------------
@@ -1845,6 +1874,14 @@ int check_fault(kdpt_ctx* c) {
 
 }  // namespace
 
+#ifdef KDPT_TAIL_PROF
+extern "C" int kdpt_debug_tail_prof(unsigned long long* out) {  // sums, then zeroes, the counters
+  const unsigned long long zero[4] = {0, 0, 0, 0};
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_tail_prof), sizeof(zero)) != hipSuccess) return -1;
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_tail_prof), zero, sizeof(zero)) == hipSuccess ? 0 : -1;
+}
+#endif
 #ifdef KDPT_SHADE_PROF
 extern "C" int kdpt_debug_shade_prof(unsigned long long* out) {  // sums, then zeroes, the counters
   const unsigned long long zero[8] = {0, 0, 0, 0, 0, 0, 0, 0};
