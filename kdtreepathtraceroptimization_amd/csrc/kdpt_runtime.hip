@@ -1182,7 +1182,7 @@ __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs
 
 // One launch per bounce and iteration: tile = ticket (tickets start the tiles in order).
 template <bool HYBRID, bool STAGE>
-__global__ __launch_bounds__(SHADE_TB) __attribute__((amdgpu_waves_per_eu(6))) void k_shade_fused(ShadeArgs A, FuseArgs F) {
+__device__ __attribute__((always_inline)) inline void shade_fused_body(const ShadeArgs& A, const FuseArgs& F) {
   const int n = A.counts[A.depth];
   // the grid covers every pixel, so past the first bounces most workgroups have no tile: exactly the first
   // ceil(n / SHADE_TB) take tickets (one contended atomic per tile, not per workgroup), the rest leave at once
@@ -1193,6 +1193,22 @@ __global__ __launch_bounds__(SHADE_TB) __attribute__((amdgpu_waves_per_eu(6))) v
   const int tile = L.tile;
   const DevScene S = stage_scene<STAGE, SHADE_TB>(A.S, L);
   shade_tile<HYBRID, STAGE, SHADE_TB>(A, F, S, tile, n, L);
+}
+
+template <bool HYBRID, bool STAGE>
+__global__ __launch_bounds__(SHADE_TB) __attribute__((amdgpu_waves_per_eu(6))) void k_shade_fused(ShadeArgs A, FuseArgs F) {
+  shade_fused_body<HYBRID, STAGE>(A, F);
+}
+
+// The same for every fused iteration of a batch in one launch (blockIdx.y = iteration): the batch's
+// shading no longer runs iteration after iteration on its stream.
+struct ShadeBatch {
+  ShadeArgs a[MAXB];
+  FuseArgs f[MAXB];
+};
+template <bool HYBRID, bool STAGE>
+__global__ __launch_bounds__(SHADE_TB) __attribute__((amdgpu_waves_per_eu(6))) void k_shade_fused_b(ShadeBatch B) {
+  shade_fused_body<HYBRID, STAGE>(B.a[blockIdx.y], B.f[blockIdx.y]);
 }
 
 // Exclusive scan of the tile counts (one workgroup; <= MAX_KEYS * ntiles entries).
@@ -1490,6 +1506,7 @@ struct kdpt_ctx {
   int* perm = nullptr;          // trace order of the next bounce
   bool trace_order = true;      // KDPT_TRACE_ORDER=0 disables (identity order)
   bool no_fuse = false;         // "shade_fused" = 0: k_shade + k_scan + k_scatter instead of k_shade_fused
+  bool shade_batch = true;      // "shade_batch": a batch's fused shading in one launch (k_shade_fused_b)
   bool zero_partial = false;    // k_gen_rays zeroes `image` (a pipeline slot's per-iteration partial image)
   int chunk_width[3] = {16, 64, 64};
   Counters* counters = nullptr;
@@ -1646,6 +1663,7 @@ int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
   c->tree_lds = p->tree_lds;
   c->trace_order = p->trace_order;
   c->no_fuse = p->no_fuse;
+  c->shade_batch = p->shade_batch;
   for (int k = 0; k < 3; k++) c->chunk_width[k] = p->chunk_width[k];
   c->counters = p->counters;
   c->total_segments = p->total_segments;
@@ -2291,6 +2309,8 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     c->S.early_walk = v;
   } else if (k == "early_leaf") {
     c->S.early_leaf = v;
+  } else if (k == "shade_batch") {
+    c->shade_batch = v != 0;
   } else if (k == "chunk_width0" || k == "chunk_width1" || k == "chunk_width2") {
     c->chunk_width[k.back() - '0'] = std::min(64, std::max(1, v));
   } else if (k == "trace_grid_frac") {
@@ -2897,6 +2917,9 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       fprintf(stderr, "[kdpt] trace depth %d done\n", depth);
     }
     if (c0->opt.testing_mode && bev) HIP_TRY(hipEventRecord((*bev)[2 * depth + 1], st));
+    ShadeBatch sbatch;
+    int nfused = 0, fused_grid = 0;
+    bool fused_hyb = false, fused_stage = false;
     for (int b = 0; b < nb; b++) {
       kdpt_ctx* c = cs[b];
       const bool sort = (iters[b] == 2);
@@ -2931,6 +2954,16 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         const bool stage = c->S.num_geoms + c->S.num_boxes <= ORDERED_GEOMS && c->S.num_materials <= STAGE_MATS;
         const bool hyb = c->opt.short_stack || c->brute;
         const int shade_grid = (c->npix + SHADE_TB - 1) / SHADE_TB;
+        if (c0->shade_batch) {  // launched below, with the batch's other fused iterations
+          sbatch.a[nfused] = a;
+          sbatch.f[nfused] = f;
+          nfused++;
+          fused_hyb = hyb;
+          fused_stage = stage;
+          fused_grid = shade_grid;
+          c->cur = nxt;
+          continue;
+        }
         if (hyb && stage) hipLaunchKernelGGL((k_shade_fused<true, true>), dim3(shade_grid), dim3(SHADE_TB), 0, st, a, f);
         else if (hyb) hipLaunchKernelGGL((k_shade_fused<true, false>), dim3(shade_grid), dim3(SHADE_TB), 0, st, a, f);
         else if (stage) hipLaunchKernelGGL((k_shade_fused<false, true>), dim3(shade_grid), dim3(SHADE_TB), 0, st, a, f);
@@ -2964,6 +2997,14 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         // no compaction, no sort: the live range stays the whole image
         HIP_TRY(hipMemcpyAsync(c->counts + depth + 1, c->counts + depth, sizeof(int), hipMemcpyDeviceToDevice, st));
       }
+    }
+    if (nfused) {  // the batch's fused iterations in one launch
+      const dim3 g(fused_grid, nfused), bl(SHADE_TB);
+      if (fused_hyb && fused_stage) hipLaunchKernelGGL((k_shade_fused_b<true, true>), g, bl, 0, st, sbatch);
+      else if (fused_hyb) hipLaunchKernelGGL((k_shade_fused_b<true, false>), g, bl, 0, st, sbatch);
+      else if (fused_stage) hipLaunchKernelGGL((k_shade_fused_b<false, true>), g, bl, 0, st, sbatch);
+      else hipLaunchKernelGGL((k_shade_fused_b<false, false>), g, bl, 0, st, sbatch);
+      HIP_TRY(hipGetLastError());
     }
     if (c0->sync_debug) {
       HIP_TRY(hipStreamSynchronize(st));
