@@ -82,11 +82,10 @@ __device__ inline unsigned int lane_prefix(unsigned long long mask) {
 // ---------------------------------------------------------------------------
 // generateRayFromCamera (src/pathtrace.cu:315-397)
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int traceDepth, PathBuf out,
-                                                  float focalLength, float dofAngle, int antialias, int* counts,
-                                                  int ncounts, int* work, int nwork,
-                                                  unsigned long long* trace_t, unsigned long long* lb, int nlb,
-                                                  float* zero_image) {
+__device__ __attribute__((always_inline)) inline void gen_rays_body(
+    const kdpt_camera& cam, int iter, int traceDepth, PathBuf out, float focalLength, float dofAngle, int antialias,
+    int* counts, int ncounts, int* work, int nwork, unsigned long long* trace_t, unsigned long long* lb, int nlb,
+    float* zero_image) {
   const int W = cam.resolution[0], H = cam.resolution[1];
   const int index = blockIdx.x * blockDim.x + threadIdx.x;
   if (index == 0) {
@@ -147,6 +146,17 @@ __global__ __launch_bounds__(256) void k_gen_rays(kdpt_camera cam, int iter, int
   out.p2[index] = make_float4(1.0f, 1.0f, 1.0f, ibits(traceDepth));
 }
 
+// Launched for a whole batch of iterations at once (k_gen_rays_b, blockIdx.y = iteration).
+struct GenIter {
+  int iter;
+  PathBuf out;
+  int* counts;
+  int* work;
+  unsigned long long* trace_t;
+  unsigned long long* lb;
+  float* zero_image;
+};
+
 // ---------------------------------------------------------------------------
 // pathTraceOneBounceKDbare (src/pathtrace.cu:1489-1662): the intersect kernel.
 //
@@ -196,6 +206,18 @@ struct TraceArgs {
   unsigned long long* trace_t;  // [4 * cap]: per bounce first block start / last block end (s_memrealtime)
                                 // of k_trace, then of k_geoms (at 2 * cap)
 };
+
+struct GenBatch {
+  GenIter it[MAXB];
+  kdpt_camera cam;
+  int traceDepth, antialias, ncounts, nwork, nlb;
+  float focalLength, dofAngle;
+};
+__global__ __launch_bounds__(256) void k_gen_rays_b(GenBatch B) {
+  const GenIter& g = B.it[blockIdx.y];
+  gen_rays_body(B.cam, g.iter, B.traceDepth, g.out, B.focalLength, B.dofAngle, B.antialias, g.counts, B.ncounts,
+                g.work, B.nwork, g.trace_t, g.lb, B.nlb, g.zero_image);
+}
 
 __device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, WaveLeafLDS* W,
                                       unsigned long long t_k0) {
@@ -296,10 +318,11 @@ __device__ __attribute__((always_inline)) inline bool prep_ray(const DevScene& S
 // is final here: it is written now, and only the rays that meet the root box are listed (cand, ccount)
 // for the intersect kernel -- whose lanes then all hold rays that actually walk the tree.
 constexpr int GEOM_BLOCK = 1024;  // k_geoms: one candidate-list atomic per 1024 paths
-__global__ __launch_bounds__(GEOM_BLOCK) void k_geoms(DevScene S, PathBuf paths, const int* counts, int depth,
-                                               int2* __restrict__ geomhit, int2* __restrict__ hits,
-                                               int* __restrict__ cand, int* __restrict__ ccount,
-                                               Counters* count_aabb, unsigned long long* gspan) {
+__device__ __attribute__((always_inline)) inline void geoms_body(const DevScene& S, PathBuf paths, const int* counts,
+                                                                 int depth, int2* __restrict__ geomhit,
+                                                                 int2* __restrict__ hits, int* __restrict__ cand,
+                                                                 int* __restrict__ ccount, Counters* count_aabb,
+                                                                 unsigned long long* gspan) {
   const int n = counts[depth];
   if ((int)(blockIdx.x * blockDim.x) >= n) return;  // uniform per block
   if (threadIdx.x == 0) atomicMin(&gspan[2 * depth], (unsigned long long)__builtin_amdgcn_s_memrealtime());
@@ -343,6 +366,27 @@ __global__ __launch_bounds__(GEOM_BLOCK) void k_geoms(DevScene S, PathBuf paths,
   __syncthreads();
   if (walk) cand[s_base + s_wcount[wv] + (int)lane_prefix(wm)] = i;
   if (threadIdx.x == 0) atomicMax(&gspan[2 * depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+}
+
+// Launched for a whole batch of iterations at once (blockIdx.y = iteration).
+struct GeomsIter {
+  PathBuf paths;
+  const int* counts;
+  int2* geomhit;
+  int2* hits;
+  int* cand;
+  int* ccount;
+};
+struct GeomsBatch {
+  DevScene S;
+  GeomsIter it[MAXB];
+  int depth;
+  Counters* count_aabb;
+  unsigned long long* gspan;
+};
+__global__ __launch_bounds__(GEOM_BLOCK) void k_geoms_b(GeomsBatch B) {
+  const GeomsIter& g = B.it[blockIdx.y];
+  geoms_body(B.S, g.paths, g.counts, B.depth, g.geomhit, g.hits, g.cand, g.ccount, B.count_aabb, B.gspan);
 }
 
 #ifdef KDPT_TAIL_PROF  // tools/build_variant.sh experiments only: intersect workgroup life / tail (ticks)
@@ -2826,14 +2870,23 @@ void launch_shade_h(kdpt_ctx* c, const ShadeArgs& a, bool compact, bool sort, hi
 int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, int stop_depth, bool count,
                  std::vector<hipEvent_t>* bev) {
   kdpt_ctx* c0 = cs[0];
-  for (int b = 0; b < nb; b++) {
-    kdpt_ctx* c = cs[b];
-    const int gen_iter = c->opt.cacherays ? 1 : iters[b];
-    c->cur = 0;
-    hipLaunchKernelGGL(k_gen_rays, dim3((c->npix + 255) / 256), dim3(256), 0, st, c->cam, gen_iter, c->traceDepth,
-                       c->buf[0], c->opt.focal_length, c->opt.dof_angle, c->opt.antialias, c->counts, c->cap + 2,
-                       c->work, c->cap, c->trace_t, c->lb, c->cap * c->ntiles,
-                       c->zero_partial ? c->image : nullptr);
+  {  // the batch's camera rays in one launch (blockIdx.y = iteration)
+    GenBatch gb;
+    gb.cam = c0->cam;
+    gb.traceDepth = c0->traceDepth;
+    gb.focalLength = c0->opt.focal_length;
+    gb.dofAngle = c0->opt.dof_angle;
+    gb.antialias = c0->opt.antialias;
+    gb.ncounts = c0->cap + 2;
+    gb.nwork = c0->cap;
+    gb.nlb = c0->cap * c0->ntiles;
+    for (int b = 0; b < nb; b++) {
+      kdpt_ctx* c = cs[b];
+      c->cur = 0;
+      gb.it[b] = GenIter{c->opt.cacherays ? 1 : iters[b], c->buf[0], c->counts, c->work, c->trace_t, c->lb,
+                         c->zero_partial ? c->image : nullptr};
+    }
+    hipLaunchKernelGGL(k_gen_rays_b, dim3((c0->npix + 255) / 256, nb), dim3(256), 0, st, gb);
     HIP_TRY(hipGetLastError());
   }
   const bool compact = c0->opt.compaction != 0;
@@ -2899,12 +2952,17 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     } else {
       // the intersect stage's first part: already done by the previous bounce's k_shade/k_scatter when it
       // ran with the hand-off (prep_ready), else here
-      for (int b = 0; b < nb && !prep_ready; b++) {
-        kdpt_ctx* c = cs[b];
-        hipLaunchKernelGGL(k_geoms, dim3((c->npix + GEOM_BLOCK - 1) / GEOM_BLOCK), dim3(GEOM_BLOCK), 0, st, c->S,
-                           c->buf[c->cur], c->counts, depth,
-                           c->geomhit, c->hits, c->cand, c->ccount, count ? c0->counters : nullptr,
-                           c0->trace_t + 2 * c0->cap);
+      if (!prep_ready) {  // the batch's iterations in one launch (blockIdx.y = iteration)
+        GeomsBatch gb;
+        gb.S = c0->S;
+        gb.depth = depth;
+        gb.count_aabb = count ? c0->counters : nullptr;
+        gb.gspan = c0->trace_t + 2 * c0->cap;
+        for (int b = 0; b < nb; b++) {
+          kdpt_ctx* c = cs[b];
+          gb.it[b] = GeomsIter{c->buf[c->cur], c->counts, c->geomhit, c->hits, c->cand, c->ccount};
+        }
+        hipLaunchKernelGGL(k_geoms_b, dim3((c0->npix + GEOM_BLOCK - 1) / GEOM_BLOCK, nb), dim3(GEOM_BLOCK), 0, st, gb);
         HIP_TRY(hipGetLastError());
       }
       launch_trace(c0, t, count, st);
