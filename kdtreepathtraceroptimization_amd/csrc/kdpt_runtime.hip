@@ -2451,7 +2451,7 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
   if (!c || count < 0 || first_iter < 1 || stride < 1) return fail(KDPT_ERR_ARG, "bad arguments");
   if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
   HIP_TRY(hipSetDevice(c->device));
-  const int depth = std::min(8, std::max(1, pipeline));
+  const int depth = std::min(16, std::max(1, pipeline));
   const int B = std::min(MAXB, std::max(1, batch));
   if (!c->accum_stream) HIP_TRY(hipStreamCreateWithFlags(&c->accum_stream, hipStreamNonBlocking));
   // the accumulation follows everything already queued on the context's own stream (reset, ...)
