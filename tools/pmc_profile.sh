@@ -13,7 +13,9 @@ ROOT=$PWD
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 BENCH=(bench.py --no-cpu-baseline "$@")
-PMC_BENCH=(bench.py --no-cpu-baseline --steps 1 --warmup 0 --spp-per-step 8 "$@")
+# the fixed step counts come last (argparse: the last one wins), so workload args pass through but the PMC
+# passes always count exactly the dispatches of the one timed step the summariser divides by
+PMC_BENCH=(bench.py --no-cpu-baseline "$@" --steps 1 --warmup 0 --spp-per-step 8)
 run() {  # name, then rocprofv3 args; a time-out or crash stops the script
   local name=$1
   shift
