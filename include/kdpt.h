@@ -230,7 +230,8 @@ int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
  * "chunk_width0..2" (16, 64, 64), "trace_grid_frac" (grid share of every intersect launch, (0, 1]),
  * "tree_global" (0; 1 = KD tree read from HBM/L2 instead of LDS), "profile_batches" (0; 1 = counting intersect kernel for kdpt_wave_profile, 2 = also its
  * per-ray node-step histogram),
- * "shade_batch" (1; 0 = one k_shade_fused launch per iteration instead of one per batch),
+ * "shade_batch" (1; 0 = one k_shade_fused launch per iteration instead of one per batch), "gen_geoms" (1;
+ * 0 = camera rays and bounce 0's k_geoms as two launches instead of one k_gen_geoms_b),
  * "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots (they are remade). */
 int kdpt_set_tuning(kdpt_ctx *ctx, const char *name, double value);
 int kdpt_destroy(kdpt_ctx *ctx);

@@ -82,10 +82,10 @@ __device__ inline unsigned int lane_prefix(unsigned long long mask) {
 // ---------------------------------------------------------------------------
 // generateRayFromCamera (src/pathtrace.cu:315-397)
 // ---------------------------------------------------------------------------
-__device__ __attribute__((always_inline)) inline void gen_rays_body(
+__device__ __attribute__((always_inline)) inline bool gen_rays_body(
     const kdpt_camera& cam, int iter, int traceDepth, PathBuf out, float focalLength, float dofAngle, int antialias,
     int* counts, int ncounts, int* work, int nwork, unsigned long long* trace_t, unsigned long long* lb, int nlb,
-    float* zero_image) {
+    float* zero_image, f3& ray_o, f3& ray_d) {
   const int W = cam.resolution[0], H = cam.resolution[1];
   const int index = blockIdx.x * blockDim.x + threadIdx.x;
   if (index == 0) {
@@ -102,7 +102,7 @@ __device__ __attribute__((always_inline)) inline void gen_rays_body(
     }
   }
   for (int e = index; e < nlb; e += gridDim.x * blockDim.x) lb[e] = 0ull;  // k_shade_fused's look-back records
-  if (index >= W * H) return;
+  if (index >= W * H) return false;
   if (zero_image) {  // batched iterations: this iteration's partial image starts at zero (no separate fill)
     zero_image[3 * index] = 0.0f;
     zero_image[3 * index + 1] = 0.0f;
@@ -144,6 +144,9 @@ __device__ __attribute__((always_inline)) inline void gen_rays_body(
   out.p0[index] = make_float4(ray.origin.x, ray.origin.y, ray.origin.z, 0.0f);
   out.p1[index] = make_float4(ray.direction.x, ray.direction.y, ray.direction.z, ibits(index));
   out.p2[index] = make_float4(1.0f, 1.0f, 1.0f, ibits(traceDepth));
+  ray_o = ray.origin;
+  ray_d = ray.direction;
+  return true;
 }
 
 // Launched for a whole batch of iterations at once (k_gen_rays_b, blockIdx.y = iteration).
@@ -215,8 +218,9 @@ struct GenBatch {
 };
 __global__ __launch_bounds__(256) void k_gen_rays_b(GenBatch B) {
   const GenIter& g = B.it[blockIdx.y];
-  gen_rays_body(B.cam, g.iter, B.traceDepth, g.out, B.focalLength, B.dofAngle, B.antialias, g.counts, B.ncounts,
-                g.work, B.nwork, g.trace_t, g.lb, B.nlb, g.zero_image);
+  f3 o, d;
+  (void)gen_rays_body(B.cam, g.iter, B.traceDepth, g.out, B.focalLength, B.dofAngle, B.antialias, g.counts,
+                      B.ncounts, g.work, B.nwork, g.trace_t, g.lb, B.nlb, g.zero_image, o, d);
 }
 
 __device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, WaveLeafLDS* W,
@@ -318,29 +322,24 @@ __device__ __attribute__((always_inline)) inline bool prep_ray(const DevScene& S
 // is final here: it is written now, and only the rays that meet the root box are listed (cand, ccount)
 // for the intersect kernel -- whose lanes then all hold rays that actually walk the tree.
 constexpr int GEOM_BLOCK = 1024;  // k_geoms: one candidate-list atomic per 1024 paths
-__device__ __attribute__((always_inline)) inline void geoms_body(const DevScene& S, PathBuf paths, const int* counts,
-                                                                 int depth, int2* __restrict__ geomhit,
-                                                                 int2* __restrict__ hits, int* __restrict__ cand,
-                                                                 int* __restrict__ ccount, Counters* count_aabb,
-                                                                 unsigned long long* gspan) {
-  const int n = counts[depth];
-  if ((int)(blockIdx.x * blockDim.x) >= n) return;  // uniform per block
-  if (threadIdx.x == 0) atomicMin(&gspan[2 * depth], (unsigned long long)__builtin_amdgcn_s_memrealtime());
-  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+// One workgroup's part: the analytic geoms + root-box test of its paths (live: the lane holds a path still
+// bouncing), the final hit record of the rays that end there, and the others appended to the candidate list
+// through *ccnt (one atomic per workgroup; a single counter hit once per wave by ~10k waves serialises for
+// ~100 us at 800x800).  Every thread of the workgroup must call it.
+__device__ __attribute__((always_inline)) inline void geoms_core(const DevScene& S, bool live, int i, f3 o, f3 d,
+                                                                 int2* __restrict__ geomhit, int2* __restrict__ hits,
+                                                                 int* __restrict__ cand, int* __restrict__ ccnt,
+                                                                 Counters* count_aabb) {
   const bool kd = S.has_obj && S.num_nodes > 0;
   bool tested = false, walk = false;  // traversed at all / goes on to the intersect kernel
-  // finished paths (compaction off) are skipped, as pathTraceOneBounce* skips them
-  if (i < n && fbits(paths.p2[i].w) > 0) {
-    const float4 q0 = paths.p0[i], q1 = paths.p1[i];
+  if (live) {
     float t_min;
     int hit;
     tested = kd;
-    walk = prep_ray(S, kd, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z), t_min, hit);
+    walk = prep_ray(S, kd, o, d, t_min, hit);
     if (walk) geomhit[i] = make_int2(fbits(t_min), hit);
     else hits[i] = make_int2(hit, -1);  // final: the analytic geoms' hit (code -1: none)
   }
-  // append the walking rays to the candidate list: one atomic per block (a single counter hit once
-  // per wave by ~10k waves serialises for ~100 us at 800x800)
   __shared__ int s_wcount[GEOM_BLOCK / 64], s_base;
   const unsigned long long wm = __ballot(walk);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
@@ -361,10 +360,30 @@ __device__ __attribute__((always_inline)) inline void geoms_body(const DevScene&
       s_wcount[w] = tot;
       tot += c;
     }
-    s_base = tot ? atomicAdd(&ccount[depth], tot) : 0;
+    s_base = tot ? atomicAdd(ccnt, tot) : 0;
   }
   __syncthreads();
   if (walk) cand[s_base + s_wcount[wv] + (int)lane_prefix(wm)] = i;
+}
+
+__device__ __attribute__((always_inline)) inline void geoms_body(const DevScene& S, PathBuf paths, const int* counts,
+                                                                 int depth, int2* __restrict__ geomhit,
+                                                                 int2* __restrict__ hits, int* __restrict__ cand,
+                                                                 int* __restrict__ ccount, Counters* count_aabb,
+                                                                 unsigned long long* gspan) {
+  const int n = counts[depth];
+  if ((int)(blockIdx.x * blockDim.x) >= n) return;  // uniform per block
+  if (threadIdx.x == 0) atomicMin(&gspan[2 * depth], (unsigned long long)__builtin_amdgcn_s_memrealtime());
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  // finished paths (compaction off) are skipped, as pathTraceOneBounce* skips them
+  const bool live = i < n && fbits(paths.p2[i].w) > 0;
+  f3 o = mk3(0, 0, 0), d = mk3(0, 0, 1);
+  if (live) {
+    const float4 q0 = paths.p0[i], q1 = paths.p1[i];
+    o = mk3(q0.x, q0.y, q0.z);
+    d = mk3(q1.x, q1.y, q1.z);
+  }
+  geoms_core(S, live, i, o, d, geomhit, hits, cand, ccount + depth, count_aabb);
   if (threadIdx.x == 0) atomicMax(&gspan[2 * depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
@@ -387,6 +406,37 @@ struct GeomsBatch {
 __global__ __launch_bounds__(GEOM_BLOCK) void k_geoms_b(GeomsBatch B) {
   const GeomsIter& g = B.it[blockIdx.y];
   geoms_body(B.S, g.paths, g.counts, B.depth, g.geomhit, g.hits, g.cand, g.ccount, B.count_aabb, B.gspan);
+}
+
+// A batch's camera rays and their bounce-0 intersect-stage first part in one launch (blockIdx.y = iteration):
+// each lane generates its pixel's ray (written out for the shading) and tests it against the analytic geoms
+// and the KD root box straight from registers.  The bounce-0 candidate counter cannot be the one the
+// generation zeroes (other workgroups of this launch already add to it), so bounce 0 counts into
+// ccount0[parity] of the context, and the launch zeroes ccount0[!parity] for the context's next use (always
+// on the same stream, so nothing still reads it).
+struct GenGeomsIter {
+  int* ccount0;       // this use's bounce-0 candidate counter
+  int* ccount0_next;  // the next use's (zeroed here)
+  int2* geomhit;
+  int2* hits;
+  int* cand;
+};
+struct GenGeomsBatch {
+  GenBatch g;
+  DevScene S;
+  GenGeomsIter it[MAXB];
+  Counters* count_aabb;
+};
+__global__ __launch_bounds__(GEOM_BLOCK) void k_gen_geoms_b(GenGeomsBatch B) {
+  const GenIter& g = B.g.it[blockIdx.y];
+  const GenGeomsIter& q = B.it[blockIdx.y];
+  f3 o = mk3(0, 0, 0), d = mk3(0, 0, 1);
+  const bool valid = gen_rays_body(B.g.cam, g.iter, B.g.traceDepth, g.out, B.g.focalLength, B.g.dofAngle,
+                                   B.g.antialias, g.counts, B.g.ncounts, g.work, B.g.nwork, g.trace_t, g.lb, B.g.nlb,
+                                   g.zero_image, o, d);
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i == 0) *q.ccount0_next = 0;
+  geoms_core(B.S, valid && B.g.traceDepth > 0, i, o, d, q.geomhit, q.hits, q.cand, q.ccount0, B.count_aabb);
 }
 
 #ifdef KDPT_TAIL_PROF  // tools/build_variant.sh experiments only: intersect workgroup life / tail (ticks)
@@ -1551,6 +1601,10 @@ struct kdpt_ctx {
   bool trace_order = true;      // KDPT_TRACE_ORDER=0 disables (identity order)
   bool no_fuse = false;         // "shade_fused" = 0: k_shade + k_scan + k_scatter instead of k_shade_fused
   bool shade_batch = true;      // "shade_batch": a batch's fused shading in one launch (k_shade_fused_b)
+  bool gen_geoms = true;        // "gen_geoms": camera rays + bounce-0 k_geoms in one launch (k_gen_geoms_b)
+  int* ccount0 = nullptr;       // [2] bounce-0 candidate counters of k_gen_geoms_b (alternating uses)
+  int gen_parity = 0;           // which of them the next use counts into
+  int* cc0_cur = nullptr;       // this use's (bounce 0 reads it instead of ccount[0])
   bool zero_partial = false;    // k_gen_rays zeroes `image` (a pipeline slot's per-iteration partial image)
   int chunk_width[3] = {16, 64, 64};
   Counters* counters = nullptr;
@@ -1656,7 +1710,7 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
   // counts[cap+3 ..]: work counters of the persistent intersect kernel
   if ((rc = dalloc(c, &c->trace_t, 4 * (size_t)c->cap))) return rc;
   HIP_TRY(hipMemset(c->trace_t, 0, sizeof(unsigned long long) * 4 * c->cap));
-  if ((rc = dalloc(c, &c->counts, 4 * (size_t)c->cap + 3)) || (rc = dalloc(c, &c->lb, (size_t)c->cap * c->ntiles)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
+  if ((rc = dalloc(c, &c->counts, 4 * (size_t)c->cap + 5)) || (rc = dalloc(c, &c->lb, (size_t)c->cap * c->ntiles)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->cand, (size_t)c->npix)) || (rc = dalloc(c, &c->prep, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->tile_ccounts, (size_t)c->ntiles)) || (rc = dalloc(c, &c->tile_coff, (size_t)c->ntiles)) ||
       (rc = dalloc(c, &c->geomhit, (size_t)c->npix)) ||
@@ -1668,12 +1722,14 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
     return rc;
   if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 3), hipHostMallocDefault) != hipSuccess)
     return fail(KDPT_ERR_HIP, "hipHostMalloc");
-  HIP_TRY(hipMemset(c->counts, 0, sizeof(int) * (4 * c->cap + 3)));
+  HIP_TRY(hipMemset(c->counts, 0, sizeof(int) * (4 * c->cap + 5)));
   HIP_TRY(hipMemset(c->lb, 0, sizeof(unsigned long long) * c->cap * c->ntiles));
   c->S.fault = c->counts + c->cap + 2;
   c->work = c->counts + c->cap + 3;
   c->ccount = c->work + c->cap;
   c->tickets = c->ccount + c->cap;
+  c->ccount0 = c->tickets + c->cap;  // 2 entries, zero
+  c->gen_parity = 0;
   return KDPT_OK;
 }
 
@@ -1708,6 +1764,7 @@ int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
   c->trace_order = p->trace_order;
   c->no_fuse = p->no_fuse;
   c->shade_batch = p->shade_batch;
+  c->gen_geoms = p->gen_geoms;
   for (int k = 0; k < 3; k++) c->chunk_width[k] = p->chunk_width[k];
   c->counters = p->counters;
   c->total_segments = p->total_segments;
@@ -2355,6 +2412,8 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     c->S.early_leaf = v;
   } else if (k == "shade_batch") {
     c->shade_batch = v != 0;
+  } else if (k == "gen_geoms") {
+    c->gen_geoms = v != 0;
   } else if (k == "chunk_width0" || k == "chunk_width1" || k == "chunk_width2") {
     c->chunk_width[k.back() - '0'] = std::min(64, std::max(1, v));
   } else if (k == "trace_grid_frac") {
@@ -2870,6 +2929,9 @@ void launch_shade_h(kdpt_ctx* c, const ShadeArgs& a, bool compact, bool sort, hi
 int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, int stop_depth, bool count,
                  std::vector<hipEvent_t>* bev) {
   kdpt_ctx* c0 = cs[0];
+  // camera rays and bounce 0's analytic geoms + root-box test in one launch (not for the brute-force and box-view
+  // intersect kernels, which have no first part)
+  const bool gen_geoms = c0->gen_geoms && !c0->brute && !c0->viz;
   {  // the batch's camera rays in one launch (blockIdx.y = iteration)
     GenBatch gb;
     gb.cam = c0->cam;
@@ -2886,7 +2948,22 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       gb.it[b] = GenIter{c->opt.cacherays ? 1 : iters[b], c->buf[0], c->counts, c->work, c->trace_t, c->lb,
                          c->zero_partial ? c->image : nullptr};
     }
-    hipLaunchKernelGGL(k_gen_rays_b, dim3((c0->npix + 255) / 256, nb), dim3(256), 0, st, gb);
+    if (gen_geoms) {
+      GenGeomsBatch gg;
+      gg.g = gb;
+      gg.S = c0->S;
+      gg.count_aabb = count ? c0->counters : nullptr;
+      for (int b = 0; b < nb; b++) {
+        kdpt_ctx* c = cs[b];
+        c->cc0_cur = c->ccount0 + c->gen_parity;
+        gg.it[b] = GenGeomsIter{c->cc0_cur, c->ccount0 + (c->gen_parity ^ 1), c->geomhit, c->hits, c->cand};
+        c->gen_parity ^= 1;
+      }
+      hipLaunchKernelGGL(k_gen_geoms_b, dim3((c0->npix + GEOM_BLOCK - 1) / GEOM_BLOCK, nb), dim3(GEOM_BLOCK), 0, st,
+                         gg);
+    } else {
+      hipLaunchKernelGGL(k_gen_rays_b, dim3((c0->npix + 255) / 256, nb), dim3(256), 0, st, gb);
+    }
     HIP_TRY(hipGetLastError());
   }
   const bool compact = c0->opt.compaction != 0;
@@ -2902,7 +2979,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       kdpt_ctx* c = cs[b < nb ? b : 0];
       t.it[b].paths = c->buf[c->cur];
       t.it[b].cand = c->cand;
-      t.it[b].ccount = c->ccount;
+      t.it[b].ccount = (depth == 0 && gen_geoms) ? c->cc0_cur : c->ccount;  // indexed by depth (0 here)
       t.it[b].geomhit = c->geomhit;
       t.it[b].hits = c->hits;
     }
@@ -2952,7 +3029,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     } else {
       // the intersect stage's first part: already done by the previous bounce's k_shade/k_scatter when it
       // ran with the hand-off (prep_ready), else here
-      if (!prep_ready) {  // the batch's iterations in one launch (blockIdx.y = iteration)
+      if (!prep_ready && !(depth == 0 && gen_geoms)) {  // the batch's iterations in one launch (blockIdx.y = iteration)
         GeomsBatch gb;
         gb.S = c0->S;
         gb.depth = depth;
@@ -3000,7 +3077,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       a.gspan = c0->trace_t + 2 * c0->cap;
       a.trace_total = b == 0 ? c->trace_total : nullptr;
       a.trace_rays = (c0->brute || c0->viz) ? nullptr : c->trace_total + 2;
-      a.ccount = c->ccount;
+      a.ccount = (depth == 0 && gen_geoms) ? c->cc0_cur : c->ccount;
       a.prep_on = prep_next ? 1 : 0;
       a.prep = c->prep;
       a.tile_ccounts = c->tile_ccounts;

@@ -299,7 +299,8 @@ def test_tuning_knobs_keep_parity(kdpt):
         with pytest.raises(kdpt.KdptError):
             pt.set_tuning("no_such_knob", 1)
     for name, val in (("tree_global", 1), ("early_walk", 0), ("early_leaf", 65), ("chunk_width0", 64),
-                      ("chunk_width1", 8), ("trace_grid_frac", 0.1), ("shade_fused", 0), ("shade_batch", 0)):
+                      ("chunk_width1", 8), ("trace_grid_frac", 0.1), ("shade_fused", 0), ("shade_batch", 0),
+                      ("gen_geoms", 0)):
         with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
             pt.set_tuning(name, val)
             pt.trace_iterations(1, 8, pipeline=2, batch=4)
