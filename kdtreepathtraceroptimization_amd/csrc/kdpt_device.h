@@ -775,38 +775,40 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     const bool hg = fastAABB ? intersectAABB_fast(o, invdir, nd.b0, nd.b1, dd)
                              : intersectAABB(o, invdir, nd.b0, nd.b1, dd);
     const bool up = curVis || !hg || dd > bz;
-    const bool leftFirst = HYBRID ? ((dpos >> min((uint32_t)nd.axis, 2u)) & 1u) != 0u : true;
-    const uint32_t fside = leftFirst ? 0u : 1u;
-    const uint32_t cl = (cb >> ((2u * Lu) & 31u)) & 3u;  // child flags of this level
-    const int first = leftFirst ? left : right, second = leftFirst ? right : left;
-    const bool hasFirst = leftFirst ? nd.hasL : nd.hasR, hasSecond = leftFirst ? nd.hasR : nd.hasL;
-    const bool takeFirst = hasFirst && !((cl >> fside) & 1u);
-    const bool takeSecond = hasSecond && !((cl >> (fside ^ 1u)) & 1u);
-    const bool descend = !up && (takeFirst || takeSecond);
-    const uint32_t nside = takeFirst ? fside : (fside ^ 1u);
-    const bool lf = !up && !descend && nd.triSize > 0;
+    // Child choice on bit masks: `has` = children present (bit 0 left, bit 1 right), `avail` = present and not
+    // yet visited at this level; the near side (fside: 0 left, 1 right) is taken when available, else the far
+    // one.  takeFirst / takeSecond of traverseKDbareShortHybrid are avail's fside / far bits, so descend =
+    // avail != 0 and the child is simply the one on side nside.
+    const uint32_t fside = HYBRID ? (((dpos >> min((uint32_t)nd.axis, 2u)) & 1u) ^ 1u) : 0u;
+    const uint32_t has = (nd.hasL ? 1u : 0u) | (nd.hasR ? 2u : 0u);
+    const uint32_t sh2 = (2u * Lu) & 31u;
+    const uint32_t avail = has & ~(cb >> sh2);  // (bits 0-1 only: has is)
+    const uint32_t nside = ((avail >> fside) & 1u) ? fside : (fside ^ 1u);
+    const bool descend = !up && avail != 0u;
+    const bool lf = !up && avail == 0u && nd.triSize > 0;
     // "Mark and stay" on a node without triangles is always followed by a trip on the same
     // node that finds it visited and climbs (same box, so same hitGeom): do both now.
-    const bool stay = !up && !descend && !lf;
+    const bool stay = !up && avail == 0u && nd.triSize <= 0;
     const bool climb = up || stay;
     if (COUNT && walk) cnt.aabb += (isRoot && curVis && !(fl & F_HITGEOM)) ? 0u : (stay ? 2u : 1u);
-    // nodeIDs[ID] = true unless descending; nodeIDs[left] = nodeIDs[right] = true when climbing
-    uint32_t ncb = cb | ((!descend && L > 0) ? (1u << vb) : 0u);
-    ncb |= climb ? ((nd.hasL ? 1u : 0u) | (nd.hasR ? 2u : 0u)) << ((2u * Lu) & 31u) : 0u;
-    const uint32_t dcb = (ncb & ~(3u << ((2u * Lu + 2u) & 31u))) | ((L == 0 && nside == 0u) ? (g << 2) : 0u);
+    // nodeIDs[ID] = true unless descending; nodeIDs[left] = nodeIDs[right] = true when climbing (neither
+    // when descending: then only the new level's child flags are cleared, and the root's own flag moves
+    // into g's slot)
+    const uint32_t ncb = descend ? ((cb & ~(3u << ((2u * Lu + 2u) & 31u))) | ((L == 0 && nside == 0u) ? (g << 2) : 0u))
+                                 : (cb | (L > 0 ? (1u << vb) : 0u) | (climb ? (has << sh2) : 0u));
     const bool runaway = guard >= S.trip_limit;
     uint32_t nfl = fl & ~(F_HITGEOM | F_LFIRST);
     nfl |= (!descend && L == 0) ? F_ROOTV : 0u;
-    nfl |= (climb && !(nd.hasL && nd.hasR)) ? F_SINK : 0u;
+    nfl |= (climb && has != 3u) ? F_SINK : 0u;
     nfl |= hg ? F_HITGEOM : 0u;
     nfl |= ((isRoot && climb) || runaway) ? F_DONE : 0u;
     nfl |= runaway ? F_FAULT : 0u;
     nfl |= lf ? F_LEAF : 0u;
-    nfl |= leftFirst ? F_LFIRST : 0u;
+    nfl |= fside == 0u ? F_LFIRST : 0u;
     if (walk) {  // commit (selects)
-      cb = descend ? dcb : ncb;
+      cb = ncb;
       ps = descend ? ((ps & ~(1u << (Lu & 31u))) | (nside << (Lu & 31u))) : ps;
-      cur = climb ? nd.parent : (descend ? (takeFirst ? first : second) : cur);
+      cur = climb ? nd.parent : (descend ? (nside ? right : left) : cur);
       L += descend ? 1 : (climb ? -1 : 0);
       guard++;
       fl = nfl;
