@@ -433,7 +433,8 @@ __device__ inline int trace_class(const DevScene& S, f3 o, f3 d) {
 //                 kernel has copied the tree there -- in LDS.  Packing:
 //     w0..w5 = min.xyz, max.xyz (float bits)
 //     w6     = left | right << 16 (0xffff = -1), or triStart for a leaf with triangles
-//     w7     = parent (16 bits, 0xffff = -1) | axis << 16 | hasTris << 18 | triSize << 19
+//     w7     = parent (16 bits, 0xffff = -1) | axis << 16 | hasTris << 18 | triSize << 19 (leaf with
+//              triangles), else hasLeft << 19 | hasRight << 20 (the node step reads them as one field)
 //   eligible when num_nodes < 65535, axis in 0..2, and every node with triangles
 //   is childless with triSize < 8192 (checked on the host, else NodesWide).
 // ---------------------------------------------------------------------------
@@ -442,6 +443,8 @@ struct NodeRec {
   float4 b1;     // max.y, max.z, -, -
   int left, right, parent, axis, triStart, triSize;  // left / right: child index when hasL / hasR
   bool hasL, hasR;
+  uint32_t has;  // hasL | hasR << 1
+  bool tris;     // triSize > 0
 };
 
 struct NodesWide {
@@ -456,9 +459,11 @@ struct NodesWide {
     r.right = q1.w;
     r.hasL = q1.z != -1;
     r.hasR = q1.w != -1;
+    r.has = (r.hasL ? 1u : 0u) | (r.hasR ? 2u : 0u);
     r.parent = q2.x;
     r.triStart = q2.y;
     r.triSize = q2.z;
+    r.tris = r.triSize > 0;
     r.axis = q2.w;
     return r;
   }
@@ -480,8 +485,10 @@ struct NodesPacked {
     const bool tris = (w7 >> 18) & 1u;
     r.left = (int)(w6 & 0xffffu);  // raw: only read when hasL / hasR
     r.right = (int)(w6 >> 16);
-    r.hasL = !tris && (w6 & 0xffffu) != 0xffffu;
-    r.hasR = !tris && (w6 >> 16) != 0xffffu;
+    r.has = tris ? 0u : (w7 >> 19) & 3u;
+    r.hasL = (r.has & 1u) != 0u;
+    r.hasR = (r.has & 2u) != 0u;
+    r.tris = tris;
     r.parent = link16(w7 & 0xffffu);
     r.axis = (int)((w7 >> 16) & 3u);
     r.triStart = (int)w6;
@@ -780,22 +787,24 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     // one.  takeFirst / takeSecond of traverseKDbareShortHybrid are avail's fside / far bits, so descend =
     // avail != 0 and the child is simply the one on side nside.
     const uint32_t fside = HYBRID ? (((dpos >> min((uint32_t)nd.axis, 2u)) & 1u) ^ 1u) : 0u;
-    const uint32_t has = (nd.hasL ? 1u : 0u) | (nd.hasR ? 2u : 0u);
+    const uint32_t has = nd.has;
     const uint32_t sh2 = (2u * Lu) & 31u;
     const uint32_t avail = has & ~(cb >> sh2);  // (bits 0-1 only: has is)
     const uint32_t nside = ((avail >> fside) & 1u) ? fside : (fside ^ 1u);
     const bool descend = !up && avail != 0u;
-    const bool lf = !up && avail == 0u && nd.triSize > 0;
+    const bool lf = !up && avail == 0u && nd.tris;
     // "Mark and stay" on a node without triangles is always followed by a trip on the same
     // node that finds it visited and climbs (same box, so same hitGeom): do both now.
-    const bool stay = !up && avail == 0u && nd.triSize <= 0;
+    const bool stay = !up && avail == 0u && !nd.tris;
     const bool climb = up || stay;
     if (COUNT && walk) cnt.aabb += (isRoot && curVis && !(fl & F_HITGEOM)) ? 0u : (stay ? 2u : 1u);
     // nodeIDs[ID] = true unless descending; nodeIDs[left] = nodeIDs[right] = true when climbing (neither
     // when descending: then only the new level's child flags are cleared, and the root's own flag moves
     // into g's slot)
-    const uint32_t ncb = descend ? ((cb & ~(3u << ((2u * Lu + 2u) & 31u))) | ((L == 0 && nside == 0u) ? (g << 2) : 0u))
-                                 : (cb | (L > 0 ? (1u << vb) : 0u) | (climb ? (has << sh2) : 0u));
+    // (both forms computed, then one select: as an if/else the compiler branches on exec masks)
+    const uint32_t cb_down = (cb & ~(3u << ((2u * Lu + 2u) & 31u))) | ((L == 0 && nside == 0u) ? (g << 2) : 0u);
+    const uint32_t cb_here = cb | (L > 0 ? (1u << vb) : 0u) | (climb ? (has << sh2) : 0u);
+    const uint32_t ncb = descend ? cb_down : cb_here;
     const bool runaway = guard >= S.trip_limit;
     uint32_t nfl = fl & ~(F_HITGEOM | F_LFIRST);
     nfl |= (!descend && L == 0) ? F_ROOTV : 0u;

@@ -1916,8 +1916,9 @@ bool pack_nodes(const kdpt_node_bare* N, int nn, const std::vector<int2>& leaf_c
     // a big leaf keeps its first cluster instead of its first triangle (its clusters carry the triangles)
     const uint32_t first = n.triIdSize >= BIG_LEAF ? (uint32_t)leaf_cl[i].x : (uint32_t)n.triIdStart;
     const uint32_t w6 = tris ? first : (l16(n.leftID) | (l16(n.rightID) << 16));
+    const uint32_t kids = (n.leftID != -1 ? 1u : 0u) | (n.rightID != -1 ? 2u : 0u);
     const uint32_t w7 = l16(n.parentID) | (axis << 16) | ((tris ? 1u : 0u) << 18) |
-                        ((tris ? (uint32_t)n.triIdSize : 0u) << 19);
+                        ((tris ? (uint32_t)n.triIdSize : kids) << 19);
     out[2 * i] = make_int4(fbits(n.mins[0]), fbits(n.mins[1]), fbits(n.mins[2]), fbits(n.maxs[0]));
     out[2 * i + 1] = make_int4(fbits(n.maxs[1]), fbits(n.maxs[2]), (int)w6, (int)w7);
   }
