@@ -527,20 +527,25 @@ struct WaveLeafLDS {
   int lastHit[64];
   int nhit[64];
   unsigned long long best[64];  // (t bits << 32) | triangle index, min
-  // count mode only, kept by lane 0 (slots: PROF_* below); last timestamp
+};
+
+// Count mode only (the counting intersect kernel allocates one per wave, the others one unused record, so
+// their LDS stays small enough for a shading workgroup to share the CU), kept by lane 0: slots PROF_*,
+// the wave's clock when its ray queue ran dry, last timestamp.
+struct WaveProf {
   unsigned long long prof[PROF_SLOTS];
-  unsigned long long tail_t0;  // count mode: the wave's clock when its ray queue ran dry
+  unsigned long long tail_t0;
   unsigned long long tlast;
 };
 
-__device__ inline void prof_add(WaveLeafLDS* W, int k, unsigned long long v) {
-  if ((threadIdx.x & 63) == 0) W->prof[k] += v;
+__device__ inline void prof_add(WaveProf* P, int k, unsigned long long v) {
+  if ((threadIdx.x & 63) == 0) P->prof[k] += v;
 }
-__device__ inline void prof_lap(WaveLeafLDS* W, int k) {  // cycles since the last lap into prof[k]
+__device__ inline void prof_lap(WaveProf* P, int k) {  // cycles since the last lap into prof[k]
   const unsigned long long now = __builtin_readcyclecounter();
   if ((threadIdx.x & 63) == 0) {
-    if (k >= 0) W->prof[k] += now - W->tlast;
-    W->tlast = now;
+    if (k >= 0) P->prof[k] += now - P->tlast;
+    P->tlast = now;
   }
 }
 
@@ -724,7 +729,8 @@ __device__ inline void wave_ray_start(const DevScene& S, WaveRay& R, f3 o, f3 d,
 // invdir finite).
 template <bool HYBRID, bool COUNT, typename NodeSrc, typename ClusterSrc>
 __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const ClusterSrc& clusters, WaveRay& R,
-                            bool fastAABB, int material_size, TraverseCounters& cnt, WaveLeafLDS* W) {
+                            bool fastAABB, int material_size, TraverseCounters& cnt, WaveLeafLDS* W,
+                            WaveProf* WP) {
   const int lane = threadIdx.x & 63;
   const f3 o = R.o, d = R.d, invdir = R.invdir;
   int& cur = R.cur;
@@ -745,7 +751,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   bool leaf = false;
   bool lfirst = true;
   int trips = 0;
-  if (COUNT) prof_lap(W, -1);
+  if (COUNT) prof_lap(WP, -1);
   // One trip = one step of the reference's loop for every lane still walking nodes.  The
   // body runs for the whole wave and commits by selects on `walk`, and the per-lane flags
   // live in one register, so a trip carries no exec-mask bookkeeping.  Exact for a
@@ -766,11 +772,11 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     if (__popcll(wmask) <= S.early_walk && __popcll(__ballot((fl & F_LEAF) != 0u)) >= S.early_leaf) break;
     if (COUNT) {
       trips += walk ? 1 : 0;
-      prof_add(W, PROF_SPARE, (unsigned long long)__popcll(wmask));  // lane-steps: SIMD efficiency
-      prof_add(W, PROF_NODE_LEAFWAIT, (unsigned long long)__popcll(__ballot((fl & F_LEAF) != 0u)));
+      prof_add(WP, PROF_SPARE, (unsigned long long)__popcll(wmask));  // lane-steps: SIMD efficiency
+      prof_add(WP, PROF_NODE_LEAFWAIT, (unsigned long long)__popcll(__ballot((fl & F_LEAF) != 0u)));
       const unsigned long long nd_done = (unsigned long long)__popcll(__ballot((fl & F_DONE) != 0u));
-      prof_add(W, PROF_NODE_DONE, nd_done);
-      if (W->tail_t0) prof_add(W, PROF_TAIL_NODE_DONE, nd_done);
+      prof_add(WP, PROF_NODE_DONE, nd_done);
+      if (WP->tail_t0) prof_add(WP, PROF_TAIL_NODE_DONE, nd_done);
     }
     const NodeRec nd = nodes(cur < 0 ? 0 : cur);
     const int left = nd.left, right = nd.right;
@@ -831,9 +837,9 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   lfirst = (fl & F_LFIRST) != 0u;
   fault = fault || (fl & F_FAULT) != 0u;
   if (COUNT) {
-    prof_lap(W, PROF_NODE_CYC);
+    prof_lap(WP, PROF_NODE_CYC);
     for (int off = 32; off > 0; off >>= 1) trips = max(trips, __shfl_xor(trips, off));
-    prof_add(W, PROF_NODE_TRIPS, (unsigned long long)trips);  // wave-level trips = the slowest lane's
+    prof_add(WP, PROF_NODE_TRIPS, (unsigned long long)trips);  // wave-level trips = the slowest lane's
   }
   if (__any(fault) && lane == 0) atomicOr(S.fault, 1);
   if (!__any(leaf)) return;
@@ -870,8 +876,8 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     W->tbase[lane] = cfirst - excl;  // cluster of pair q = tbase[owner] + q
     wave_lds_sync();
     if (COUNT) {
-      prof_add(W, PROF_BIG_LEAVES, (unsigned long long)__popcll(__ballot(big)));
-      prof_add(W, PROF_BIG_CLUSTERS, (unsigned long long)P);
+      prof_add(WP, PROF_BIG_LEAVES, (unsigned long long)__popcll(__ballot(big)));
+      prof_add(WP, PROF_BIG_CLUSTERS, (unsigned long long)P);
     }
     unsigned long long k_pass = 0ull, k_best = ~0ull;
     int k_lasthit = -1, k_nhit = 0;
@@ -903,7 +909,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
           const int ctn = __builtin_amdgcn_readlane(c, sn) * 64 + lane;
           Tn = TriData{S.c_v0[ctn], S.c_e1[ctn], S.c_e2[ctn]};
         }
-        if (COUNT) prof_add(W, PROF_BIG_SWEEPS, 1);
+        if (COUNT) prof_add(WP, PROF_BIG_SWEEPS, 1);
         const int j = __builtin_amdgcn_readlane(own, s);  // the cluster's ray: lane j's, wave-uniform
         const f3 jo = mk3(readlane_f(o.x, j), readlane_f(o.y, j), readlane_f(o.z, j));
         const f3 jd = mk3(readlane_f(d.x, j), readlane_f(d.y, j), readlane_f(d.z, j));
@@ -912,8 +918,8 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         const int r = tri_test_v(T, jo, jd, bx, by, bzk);
         const unsigned long long m1 = __ballot(r >= 1);
         if (COUNT && m1) {
-          prof_add(W, PROF_BIG_PASS, 1);
-          prof_add(W, PROF_BIG_MULTI, (m1 & (m1 - 1)) ? 1 : 0);
+          prof_add(WP, PROF_BIG_PASS, 1);
+          prof_add(WP, PROF_BIG_MULTI, (m1 & (m1 - 1)) ? 1 : 0);
         }
         if (m1) {
           const unsigned long long pk =
@@ -953,12 +959,12 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       r_best = k_best;
     }
   }
-  if (COUNT) prof_lap(W, PROF_BIG_CYC);
+  if (COUNT) prof_lap(WP, PROF_BIG_CYC);
   // (b) small leaves: the items are triangles, every (ray, triangle) pair tested by one lane; results
   // recombine through LDS atomics on the owner's slots
   const int sz = (leaf && !big) ? lsize : 0;
   if (__any(sz > 0)) {
-    if (COUNT) prof_add(W, PROF_SMALL_PHASES, 1);
+    if (COUNT) prof_add(WP, PROF_SMALL_PHASES, 1);
     const int incl = wave_incl_scan<false>(sz);
     const int P = __builtin_amdgcn_readlane(incl, 63);
     const int excl = incl - sz;
@@ -969,8 +975,8 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     W->best[lane] = ~0ull;
     wave_lds_sync();
     if (COUNT) {
-      prof_add(W, PROF_SMALL_ROUNDS, (unsigned long long)((P + 63) / 64));
-      prof_add(W, PROF_SMALL_PAIRS, (unsigned long long)P);
+      prof_add(WP, PROF_SMALL_ROUNDS, (unsigned long long)((P + 63) / 64));
+      prof_add(WP, PROF_SMALL_PAIRS, (unsigned long long)P);
     }
     // the next round's owners are found and its triangles loaded while the current round is tested
     int carry = 0;
@@ -1015,7 +1021,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     }
     wave_lds_sync();  // the LDS slots are rewritten by the next leaf phase
   }
-  if (COUNT) prof_lap(W, PROF_SMALL_CYC);
+  if (COUNT) prof_lap(WP, PROF_SMALL_CYC);
   if (leaf) {
     if (COUNT) cnt.tri += lsize;
     if (r_pass > 0) bz = r_bz;
@@ -1059,7 +1065,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     cur = lparent;
     L--;
   }
-  if (COUNT) prof_lap(W, PROF_FINAL_CYC);
+  if (COUNT) prof_lap(WP, PROF_FINAL_CYC);
 }
 #endif  // HIP
 

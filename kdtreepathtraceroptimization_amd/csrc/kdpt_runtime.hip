@@ -223,7 +223,7 @@ __global__ __launch_bounds__(256) void k_gen_rays_b(GenBatch B) {
                       B.ncounts, g.work, B.nwork, g.trace_t, g.lb, B.nlb, g.zero_image, o, d);
 }
 
-__device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, WaveLeafLDS* W,
+__device__ inline void flush_counters(Counters* C, const TraverseCounters& cnt, WaveProf* W,
                                       unsigned long long t_k0) {
   unsigned int a = cnt.aabb, tr = cnt.tri, hi = cnt.hit;
   for (int off = 32; off > 0; off >>= 1) {
@@ -446,11 +446,22 @@ __device__ unsigned long long g_tail_prof[4];
 // KD traversal of every live path.  Each lane holds one ray; whenever rays finish, the idle lanes take
 // the next paths of the bounce from a device counter, so a wave stays full until the bounce runs out
 // of paths (the per-ray algorithm is unchanged -- only which lane runs it, and when).
+// Compiled for 5 waves per SIMD although a workgroup brings only 4 (its LDS tree copy keeps it alone on the
+// CU): the cap (96 VGPRs instead of 108, a few spilled to scratch outside the hot loops) leaves 128 VGPRs per
+// SIMD, room for a fused-shading wave of another batch on the same CU while the traversal runs -- and its LDS
+// (WaveProf only in the counting kernel) leaves room for that workgroup's 4.2 KB.  A/B +2.8 %.
+#ifndef KDPT_TRACE_WAVES
+#define KDPT_TRACE_WAVES 5  // tools/build_variant.sh experiments
+#endif
+// (only with the tree in LDS: the 256-thread workgroups of the other modes share CUs anyway, and the C5
+// icosphere, whose tree lives in HBM, lost 3.5 % to the cap)
+#define KDPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(MODE == TREE_LDS ? KDPT_TRACE_WAVES : 1)))
 template <bool HYBRID, bool COUNT, int MODE>
-__global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
+__global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(TraceArgs A) {
   constexpr int TB = trace_block<MODE>();
   extern __shared__ int4 s_tree[];
   __shared__ WaveLeafLDS s_leaf[TB / 64];
+  __shared__ WaveProf s_prof[COUNT ? TB / 64 : 1];
   const DevScene& S = A.S;
   int pre[MAXB + 1];  // the batch's paths, concatenated: iteration b owns queue slots [pre[b], pre[b+1])
   pre[0] = 0;
@@ -470,8 +481,9 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
   }
   const int lane = threadIdx.x & 63;
   WaveLeafLDS* W = &s_leaf[threadIdx.x >> 6];
-  if (COUNT && lane < PROF_SLOTS) W->prof[lane] = 0;
-  if (COUNT && lane == 0) W->tail_t0 = 0;
+  WaveProf* P = &s_prof[COUNT ? (threadIdx.x >> 6) : 0];
+  if (COUNT && lane < PROF_SLOTS) P->prof[lane] = 0;
+  if (COUNT && lane == 0) P->tail_t0 = 0;
   W->slot[lane] = 0;  // pair_owner's invariant
   // launch duration on the device clock (first block start .. last block end); the HIP events around
   // the launch also count time spent queued behind other streams' kernels when iterations overlap
@@ -516,7 +528,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
       break;
     }
     // ---- refill idle lanes ----
-    if (COUNT) prof_lap(W, -1);
+    if (COUNT) prof_lap(P, -1);
     const unsigned long long im = exhausted ? 0ull : __ballot(pidx < 0);
     if (im) {
       const int p = (int)lane_prefix(im);
@@ -532,7 +544,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
         k = base + p;
         exhausted = base + __popcll(im) >= n;  // the counter only grows: later rounds find nothing
       }
-      if (COUNT && exhausted && lane == 0 && !W->tail_t0) W->tail_t0 = __builtin_readcyclecounter();
+      if (COUNT && exhausted && lane == 0 && !P->tail_t0) P->tail_t0 = __builtin_readcyclecounter();
 #ifdef KDPT_TAIL_PROF
       if (exhausted && !tex_seen) tex_seen = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -561,7 +573,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
         wave_ray_start(S, R, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z), u2f((uint32_t)gh.x), gh.y, W);
       }
     }
-    if (COUNT) prof_lap(W, PROF_SETUP_CYC);
+    if (COUNT) prof_lap(P, PROF_SETUP_CYC);
     const bool busy = pidx >= 0 && !R.done;
     if (__any(busy)) {
       const bool fastAABB = __all(!busy || (fabsf(R.invdir.x) < FLT_INFV && fabsf(R.invdir.y) < FLT_INFV &&
@@ -569,13 +581,13 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
       if (MODE == TREE_LDS)
         trace_phase<HYBRID, COUNT>(S, NodesPacked{s_tree},
                                    ClustersInterleaved{reinterpret_cast<const float4*>(s_tree + 2 * S.num_nodes)}, R,
-                                   fastAABB, S.num_materials, cnt, W);
+                                   fastAABB, S.num_materials, cnt, W, P);
       else if (MODE == TREE_PACKED)
         trace_phase<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
-                                   S.num_materials, cnt, W);
+                                   S.num_materials, cnt, W, P);
       else
         trace_phase<HYBRID, COUNT>(S, NodesWide{S.nodes}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
-                                   S.num_materials, cnt, W);
+                                   S.num_materials, cnt, W, P);
     }
     // ---- finished rays: their hit record (what ShadeableIntersection would carry) ----
     if (pidx >= 0 && R.done) {
@@ -611,9 +623,9 @@ __global__ __launch_bounds__(trace_block<MODE>()) void k_trace(TraceArgs A) {
     }
   }
   if (COUNT) {
-    prof_lap(W, PROF_POST_CYC);
-    if (lane == 0 && W->tail_t0) W->prof[PROF_TAIL_CYC] += __builtin_readcyclecounter() - W->tail_t0;
-    flush_counters(A.counters, cnt, W, t_k0);
+    prof_lap(P, PROF_POST_CYC);
+    if (lane == 0 && P->tail_t0) P->prof[PROF_TAIL_CYC] += __builtin_readcyclecounter() - P->tail_t0;
+    flush_counters(A.counters, cnt, P, t_k0);
     if (lane == 0) {
       const unsigned long long us10 = (__builtin_amdgcn_s_memrealtime() - rt0) / 1000;  // 100 MHz ticks
       atomicAdd(&A.counters->life[us10 < 63 ? us10 : 63], 1ull);
@@ -1122,6 +1134,9 @@ __device__ unsigned long long g_shade_prof[8];
 #ifndef KDPT_SHADE_TB
 #define KDPT_SHADE_TB 256  // tools/build_variant.sh experiments only
 #endif
+#ifndef KDPT_SHADE_WAVES
+#define KDPT_SHADE_WAVES 6  // fused shading: waves per SIMD it is compiled for (caps its VGPRs at 80)
+#endif
 constexpr int SHADE_TB = KDPT_SHADE_TB;  // paths per fused-shading workgroup (one tile ticket each)
 
 // The LDS a shading workgroup uses: staged geoms/materials and the per-tile compaction scratch.
@@ -1290,7 +1305,7 @@ __device__ __attribute__((always_inline)) inline void shade_fused_body(const Sha
 }
 
 template <bool HYBRID, bool STAGE>
-__global__ __launch_bounds__(SHADE_TB) __attribute__((amdgpu_waves_per_eu(6))) void k_shade_fused(ShadeArgs A, FuseArgs F) {
+__global__ __launch_bounds__(SHADE_TB) __attribute__((amdgpu_waves_per_eu(KDPT_SHADE_WAVES))) void k_shade_fused(ShadeArgs A, FuseArgs F) {
   shade_fused_body<HYBRID, STAGE>(A, F);
 }
 
@@ -1301,7 +1316,7 @@ struct ShadeBatch {
   FuseArgs f[MAXB];
 };
 template <bool HYBRID, bool STAGE>
-__global__ __launch_bounds__(SHADE_TB) __attribute__((amdgpu_waves_per_eu(6))) void k_shade_fused_b(ShadeBatch B) {
+__global__ __launch_bounds__(SHADE_TB) __attribute__((amdgpu_waves_per_eu(KDPT_SHADE_WAVES))) void k_shade_fused_b(ShadeBatch B) {
   shade_fused_body<HYBRID, STAGE>(B.a[blockIdx.y], B.f[blockIdx.y]);
 }
 
@@ -1940,7 +1955,8 @@ int setup_trace(kdpt_ctx* c) {
   HIP_TRY(hipGetDeviceProperties(&prop, c->device));
   c->tree_mode = c->S.pnodes ? TREE_PACKED : TREE_WIDE;
   c->tree_lds = 0;
-  const size_t static_lds = sizeof(WaveLeafLDS) * (TRACE_BLOCK / 64);
+  // (the counting kernel's per-wave WaveProf too: the tree must fit next to either kernel's static part)
+  const size_t static_lds = (sizeof(WaveLeafLDS) + sizeof(WaveProf)) * (TRACE_BLOCK / 64);
   const size_t tree_bytes = 32 * (size_t)c->S.num_nodes + 32 * (size_t)c->S.num_clusters;  // + cluster boxes
   const size_t lds_max = prop.sharedMemPerBlock > 0 ? prop.sharedMemPerBlock : 65536;
   if (c->S.pnodes && static_lds + tree_bytes <= lds_max && !c->force_global_tree) {

@@ -29,11 +29,17 @@ def _report():
 HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_shade_fused": 6, "k_geoms": 4, "k_gen_rays": 4}
 
 
+# k_trace is compiled for 5 waves per SIMD (96 VGPRs) so that a shading wave of another batch fits beside its
+# 4 waves: the few values that no longer fit are spilled once at the start and reloaded once per round (a node
+# phase + a leaf phase), outside the node and leaf loops; measured +2.8 % overall (profiles/r02_ab_log.md)
+SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 32, "k_traceILb0ELb0ELi2E": 32}
+
+
 @pytest.mark.parametrize("frag", sorted(HOT))
 def test_hot_kernels_no_scratch(kdpt, frag):
     rep = _report()
     ks = [k for k in rep if frag in k]
     assert ks, frag
     for k in ks:
-        assert rep[k].get("ScratchSize", 0) == 0, (k, rep[k])
+        assert rep[k].get("ScratchSize", 0) <= SCRATCH_OK.get(frag, 0), (k, rep[k])
         assert rep[k].get("Occupancy", 0) >= HOT[frag], (k, rep[k])
