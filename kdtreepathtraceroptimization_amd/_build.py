@@ -63,7 +63,10 @@ def build(force: bool = False) -> str:
     # the per-kernel resource report (VGPRs, scratch, occupancy) goes to the build log, which
     # tests/test_build_resources.py checks: a hot kernel that starts spilling or calling out-of-line
     # functions (scratch > 0) fails the CPU suite instead of silently losing half its occupancy
-    _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-Rpass-analysis=kernel-resource-usage", "-c",
+    # the max-ILP machine scheduler: A/B +1.2 % (k_trace launch -1 %), profiles/r02_ab_log.md; it reorders
+    # instructions only, so the results stay bit-identical
+    _run([HIPCC, f"--offload-arch={ARCH}", *COMMON, "-mllvm", "-amdgpu-sched-strategy=max-ilp",
+          "-Rpass-analysis=kernel-resource-usage", "-c",
           os.path.join(CSRC, "kdpt_runtime.hip"), "-o", dev_obj], log=RESOURCE_LOG)
     tmp = LIB + ".tmp"
     _run([HIPCC, f"--offload-arch={ARCH}", "-shared", "-fPIC", "-o", tmp, dev_obj, kd_obj, host_obj, io_obj])

@@ -32,7 +32,9 @@ HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_shade_fused": 6,
 # k_trace is compiled for 5 waves per SIMD (96 VGPRs) so that a shading wave of another batch fits beside its
 # 4 waves: the few values that no longer fit are spilled once at the start and reloaded once per round (a node
 # phase + a leaf phase), outside the node and leaf loops; measured +2.8 % overall (profiles/r02_ab_log.md)
-SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 32, "k_traceILb0ELb0ELi2E": 32}
+# The max-ILP machine scheduler (the runtime's build flags) spills up to 20 B of the fused shading at its
+# 80-VGPR cap; the build with it measured +1.2 % over the default scheduler's spill-free one (profiles/r02_ab_log.md)
+SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 32, "k_traceILb0ELb0ELi2E": 32, "k_shade_fused": 20}
 
 
 @pytest.mark.parametrize("frag", sorted(HOT))
