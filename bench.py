@@ -3,12 +3,13 @@
 Metric (BASELINE.json): Mrays/s at 800x800, depth 8, cornell + dragon (dragon_5.obj: the only dragon mesh
 present -- cornell9.txt does not exist), plus ms per iteration.
 
-A step is one frame of `--spp-per-step` samples per pixel (default 16): that many iterations of the whole
+A step is one frame of `--spp-per-step` samples per pixel (default 256): that many iterations of the whole
 hot path (camera rays -> up to 8 x [intersect + KD traversal + scatter + shade + gather + stable
 compaction]), each a distinct global iteration number (its own RNG seed).  Mrays/s = path segments
 launched into the intersect stage, summed over all ranks, / the max-over-ranks wall time of the K timed
-steps.  Iterations stay in flight across the frame (kdpt_trace_iterations), so a frame of 16 samples
-keeps the GPU at steady state; `ms_per_iteration` is reported beside `ms_per_step`.
+steps.  Iterations stay in flight across the frame (kdpt_trace_iterations), so the GPU stays at steady
+state; `ms_per_iteration` is reported beside `ms_per_step`.  256 samples per step make the driver's
+`--steps 20 --warmup 5` timed region about 2.5 s of GPU work (5 120 iterations).
 
 Multi-GPU (one process per GPU, `torch.distributed.run`): samples per pixel shard across ranks (rank r
 renders global iterations r+1, r+1+N, ...: weak scaling) and the float3 accumulation images are summed on
@@ -19,7 +20,8 @@ bound by VALU issue and latency, not HBM (its tree lives in LDS, its triangles i
 roofline is VALU issue: peak = 256 CUs x 4 SIMDs x 1/2 wave64 VALU instruction per clock x 2.4 GHz.
 achieved = k_trace's VALU wave-instructions per launch / (launch duration x the grid share the launch ran
 on): the instructions per k_trace ray come from rocprofv3 SQ_INSTS_VALU of the same kernel sources
-(profiles/pmc_<workload>.json, matched by a hash of the kernel sources -- null when stale), the rays per
+(profiles/pmc_<workload>.json, matched by the hash of the kernel sources + compile flags AND the hash of
+the library's gfx950 code objects (.hip_fatbin) -- null when either differs), the rays per
 launch and the launch duration are measured live (device counters, s_memrealtime).  traffic = HBM bytes
 per launch from the same profile (FETCH_SIZE x 2, the gfx950 correction of MI355X_MICROARCH.md, +
 WRITE_SIZE), scaled to the live rays per launch.
@@ -27,7 +29,6 @@ WRITE_SIZE), scaled to the live rays per launch.
 from __future__ import annotations
 
 import argparse
-import hashlib
 import json
 import os
 import sys
@@ -45,7 +46,6 @@ METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 # VALU issue: 256 CUs x 4 SIMD-32 x one wave64 instruction per 2 clocks x 2.4 GHz (MI355X_MICROARCH.md)
 VALU_PEAK_GINST = 256 * 4 * 0.5 * 2.4
-KERNEL_SOURCES = ["kdpt_device.h", "kdpt_math.h", "kdpt_runtime.hip", "glibc_sincostab.h"]
 
 
 def parse():
@@ -53,7 +53,7 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--spp-per-step", type=int, default=16, help="iterations (samples per pixel) per step")
+    ap.add_argument("--spp-per-step", type=int, default=256, help="iterations (samples per pixel) per step")
     ap.add_argument("--mesh", default="dragon_5")
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--res", type=int, nargs=2, default=(800, 800))
@@ -62,7 +62,8 @@ def parse():
     ap.add_argument("--bounce-cap", type=int, default=8,
                     help="bounces per iteration (8 = the reference's `depth > 7`; 16 for the C5 stress config)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--cpu-repeats", type=int, default=3, help="CPU-baseline repeats (median and spread)")
+    ap.add_argument("--cpu-iters", type=int, default=8, help="iterations per repeat of the multi-thread CPU leg")
     ap.add_argument("--pipeline", type=int, default=8,
                     help="batches in flight (kdpt_trace_iterations; bit-identical to one at a time)")
     ap.add_argument("--batch", type=int, default=4, help="iterations sharing each intersect launch (<= 4)")
@@ -71,16 +72,23 @@ def parse():
                          "N > 1 path with several ranks sharing one GPU")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                     help="kdpt_set_tuning knob for A/B runs (not for reported numbers)")
+    ap.add_argument("--dump-image", default=None, help="rank 0 saves the reduced float3 image of the timed "
+                    "iterations here (.npy; tests/test_gpu_sharded.py checks the N > 1 path with it)")
     ap.add_argument("--pmc-profile", default=None, help="profile JSON for the VALU roofline (default: "
                     "profiles/pmc_<scene>_<mesh>_<W>x<H>.json)")
     return ap.parse_args()
 
 
 def kernel_source_hash() -> str:
-    h = hashlib.sha256()
-    for f in KERNEL_SOURCES:
-        h.update(open(os.path.join(ROOT, "kdtreepathtraceroptimization_amd", "csrc", f), "rb").read())
-    return h.hexdigest()[:16]
+    """Kernel sources + device compile flags (the build recipe of the code object)."""
+    from kdtreepathtraceroptimization_amd import _build
+    return _build.kernel_source_sha()
+
+
+def code_object_hash() -> str | None:
+    """The gfx950 code objects of the library this process loads (KDPT_LIBRARY or the in-tree build)."""
+    from kdtreepathtraceroptimization_amd import _build, runtime
+    return _build.code_object_sha(runtime.LIB_PATH)
 
 
 def host_info():
@@ -97,10 +105,13 @@ def host_info():
     return {"cpu_model": model, "nproc": os.cpu_count(), "affinity_cpus": aff, "omp_num_threads": omp}
 
 
-def cpu_baseline(args, threads=None, seconds=None):
+def cpu_baseline(args, threads=None, iters=None):
     """The oracle (plain-C port of the reference path, OpenMP over paths) on this host's cores, on a
-    bounded sample of the same workload.  Threads: every CPU this process may run on, capped by
-    OMP_NUM_THREADS when the environment sets it (the GPU box allots 16 host CPUs per GPU and sets it)."""
+    bounded sample of the same workload: `repeats` runs of `iters` consecutive iterations each, median and
+    spread reported.  Threads: the CPUs this process may run on, capped by OMP_NUM_THREADS when the
+    environment sets it (the GPU box allots 16 host CPUs per GPU and sets it to 16).  `cpu_util` = process
+    CPU time / (wall x threads): below 1 the host was shared or the threads stalled, which is how a run-to-run
+    drift shows itself."""
     sys.path.insert(0, os.path.join(ROOT, "tests"))
     import oracle_lib
     from kdtreepathtraceroptimization_amd.fixtures import load_fixture_scene
@@ -109,19 +120,30 @@ def cpu_baseline(args, threads=None, seconds=None):
         threads = info["affinity_cpus"]
         if info["omp_num_threads"]:
             threads = max(1, min(threads, int(info["omp_num_threads"])))
-    seconds = args.cpu_seconds if seconds is None else seconds
+    iters = args.cpu_iters if iters is None else iters
     s = oracle_lib.OracleScene.from_description(
         load_fixture_scene(args.scene, args.mesh, res=tuple(args.res), depth=args.depth))
-    seg, t, it = 0, 0.0, 3
-    while t < seconds and it < 3 + 64:
-        t0 = time.perf_counter()
-        _, st = s.render(it, 1, nthreads=threads, shortstack=0 if args.bare else 1, bounce_cap=args.bounce_cap)
-        t += time.perf_counter() - t0
-        seg += st.segments
-        it += 1
-    return {"value": round(seg / t / 1e6, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
-            "sample": f"oracle (plain-C restatement of the reference's host-side kernels), {it - 3} iteration(s) "
-                      f"3..{it - 1} of the same workload, {t:.1f} s, OpenMP over paths, {threads} thread(s)",
+    runs, utils = [], []
+    it = 3
+    for _ in range(max(1, args.cpu_repeats)):
+        seg, t, c = 0, 0.0, 0.0
+        for _ in range(iters):
+            t0, c0 = time.perf_counter(), time.process_time()
+            _, st = s.render(it, 1, nthreads=threads, shortstack=0 if args.bare else 1, bounce_cap=args.bounce_cap)
+            t += time.perf_counter() - t0
+            c += time.process_time() - c0
+            seg += st.segments
+            it += 1
+        runs.append(seg / t / 1e6)
+        utils.append(c / (t * threads))
+    runs_sorted = sorted(runs)
+    med = runs_sorted[len(runs) // 2]
+    return {"value": round(med, 4), "unit": "Mrays/s", "cores": threads, "kind": "port",
+            "repeats": [round(r, 4) for r in runs], "spread": round((max(runs) - min(runs)) / med, 4),
+            "cpu_util": [round(u, 3) for u in utils],
+            "sample": f"oracle (plain-C restatement of the reference's host-side kernels), median of {len(runs)} "
+                      f"repeats of {iters} iteration(s) each (iterations 3..{it - 1}) of the same workload, "
+                      f"OpenMP over paths, {threads} thread(s)",
             "host": info}
 
 
@@ -131,14 +153,16 @@ def valu_roofline(args, W, H, rays_per_launch, launch_ms, share):
     out = {"bound": "valu-issue", "unit": "G VALU wave-instructions/s", "peak": VALU_PEAK_GINST,
            "achieved": None, "frac": None, "traffic": None, "kernel": "k_trace",
            "pmc_source": os.path.relpath(path, ROOT)}
-    src = kernel_source_hash()
+    src, cos = kernel_source_hash(), code_object_hash()
+    out["kernel_source_sha"], out["code_object_sha"] = src, cos
     if not os.path.exists(path):
         out["note"] = "no PMC profile for this workload"
         return out
     prof = json.load(open(path))
     k = prof.get("kernels", {}).get("k_trace")
-    if prof.get("kernel_source_sha") != src or not k:
-        out["note"] = f"PMC profile is for kernel sources {prof.get('kernel_source_sha')}, not {src}: stale"
+    if prof.get("kernel_source_sha") != src or prof.get("code_object_sha") != cos or not k:
+        out["note"] = (f"PMC profile is for kernel build {prof.get('kernel_source_sha')} / code object "
+                       f"{prof.get('code_object_sha')}, not {src} / {cos}: stale")
         return out
     inst = k["valu_per_ray"] * rays_per_launch
     eff_s = launch_ms * 1e-3 * share  # the launch ran on `share` of the chip's CUs
@@ -151,7 +175,7 @@ def valu_roofline(args, W, H, rays_per_launch, launch_ms, share):
     out["valu_inst_per_launch"] = round(inst)
     out["valu_per_ray"] = k["valu_per_ray"]
     out["pmc_exclusive_valu_frac"] = k.get("valu_busy_frac")
-    out["kernel_source_sha"] = src
+    out["pmc_git_head"] = prof.get("git_head")
     return out
 
 
@@ -227,6 +251,9 @@ def main():
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         dt = float(tmax[0])
         seg, rays, kernel_ms, launches = int(tsum[0]), int(tsum[1]), float(tsum[2]), int(tsum[3])
+    if rank == 0 and args.dump_image:
+        import numpy as np
+        np.save(args.dump_image, accum.cpu().numpy())
     if rank != 0:
         pt.close()
         if dist:
@@ -287,7 +314,7 @@ def main():
     if world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(args)
         # SURVEY 8(d) / BASELINE.md 3: the same oracle on one core as well
-        out["cpu_baseline_1core"] = cpu_baseline(args, threads=1, seconds=args.cpu_seconds / 2)
+        out["cpu_baseline_1core"] = cpu_baseline(args, threads=1, iters=1)
     pt.close()
     if dist:
         dist.destroy_process_group()

@@ -264,6 +264,11 @@ int kdpt_wave_profile(kdpt_ctx *ctx, unsigned long long *out, int n);
 /* Device-math known answers: sinf/cosf/pow-5 Fresnel/u01 evaluated by the gfx950 code. */
 int kdpt_selftest_math(const float *x, int n, float *sin_out, float *cos_out);
 int kdpt_selftest_rng(const int *iter_idx_depth, int n, int k, float *u_out);
+/* The first k uniform draws (n x k) of thrust::default_random_engine + uniform_real_distribution<float>
+ * as the device restates them, per input: mode 0 makeSeededRandomEngine(iter, index, depth) of int
+ * triples (src/pathtrace.cu:62-66), 1 the camera jitter's engine(utilhash(iter)) (src/pathtrace.cu:334),
+ * 2 engine(seed) of raw uint32 seeds.  Pinned to rocThrust by tests/golden/ref_pins.json. */
+int kdpt_selftest_rng_draws(int mode, const uint32_t *in, int n, int k, float *out);
 int kdpt_selftest_fresnel(const float *cosines, int n, float ior, float *f_out);
 /* The glm pieces on the path (kdpt_device.h glm_kat, vendored glm 0.9.6.3 restated): fn 0
  * intersectRayTriangle (15 floats in -> {passed, bary.xyz}; `out` holds sentinels on entry, kept where

@@ -1558,6 +1558,13 @@ __global__ void k_selftest_rng(const int* iid, int n, int k, float* u) {
   for (int j = 0; j <= k; j++) v = u01(r);
   u[i] = v;
 }
+__global__ void k_selftest_rng_draws(int mode, const uint32_t* in, int n, int k, float* out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n) return;
+  Rng r = mode == 0 ? seeded_rng((int)in[3 * i], (int)in[3 * i + 1], (int)in[3 * i + 2])
+        : mode == 1 ? rng_seed(utilhash(in[i])) : rng_seed(in[i]);
+  for (int j = 0; j < k; j++) out[(size_t)i * k + j] = u01(r);
+}
 __global__ void k_selftest_glm(int fn, const float* in, int n, float* out) {
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i >= n) return;
@@ -2876,6 +2883,31 @@ int kdpt_selftest_rng(const int* iid, int n, int k, float* u) {
   HIP_TRY(hipMemcpy(u, du, sizeof(float) * n, hipMemcpyDeviceToHost));
   (void)hipFree(di); (void)hipFree(du);
   return KDPT_OK;
+}
+
+int kdpt_selftest_rng_draws(int mode, const uint32_t* in, int n, int k, float* out) {
+  if (mode < 0 || mode > 2 || n < 0 || k < 0 || (n && k && (!in || !out)))
+    return fail(KDPT_ERR_ARG, "bad rng selftest arguments");
+  if (!n || !k) return KDPT_OK;
+  const size_t nin = (size_t)n * (mode == 0 ? 3 : 1), nout = (size_t)n * k;
+  uint32_t* di;
+  float* dout;
+  HIP_TRY(hipMalloc((void**)&di, sizeof(uint32_t) * nin));
+  if (hipMalloc((void**)&dout, sizeof(float) * nout) != hipSuccess) {
+    (void)hipFree(di);
+    return fail(KDPT_ERR_HIP, "hipMalloc failed");
+  }
+  int rc = KDPT_OK;
+  if (hipMemcpy(di, in, sizeof(uint32_t) * nin, hipMemcpyHostToDevice) != hipSuccess) rc = KDPT_ERR_HIP;
+  if (rc == KDPT_OK) {
+    hipLaunchKernelGGL(k_selftest_rng_draws, dim3((n + 255) / 256), dim3(256), 0, 0, mode, di, n, k, dout);
+    if (hipGetLastError() != hipSuccess ||
+        hipMemcpy(out, dout, sizeof(float) * nout, hipMemcpyDeviceToHost) != hipSuccess)
+      rc = KDPT_ERR_HIP;
+  }
+  (void)hipFree(di);
+  (void)hipFree(dout);
+  return rc == KDPT_OK ? KDPT_OK : fail(rc, "rng selftest failed");
 }
 
 int kdpt_selftest_glm(int fn, const float* in, int n, float* out) {

@@ -109,7 +109,7 @@ assert C.sizeof(NodeBare) == 64 and C.sizeof(TriBare) == 76 and C.sizeof(PathSeg
 EXPORTS = [
     "kdpt_default_options", "kdpt_create", "kdpt_trace_iteration", "kdpt_trace_iteration_async", "kdpt_trace_iterations", "kdpt_synchronize",
     "kdpt_read_image", "kdpt_write_pbo", "kdpt_reset", "kdpt_get_stats", "kdpt_destroy", "kdpt_last_error",
-    "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_count_split", "kdpt_wave_profile", "kdpt_selftest_math", "kdpt_selftest_rng",
+    "kdpt_image_device_ptr", "kdpt_debug_paths", "kdpt_count_iteration", "kdpt_count_split", "kdpt_wave_profile", "kdpt_selftest_math", "kdpt_selftest_rng", "kdpt_selftest_rng_draws",
     "kdpt_selftest_fresnel", "kdpt_selftest_libm", "kdpt_selftest_libm_digest", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
     "kdpt_save_rgb8", "kdpt_save_png", "kdpt_save_hdr", "kdpt_png_encode", "kdpt_write_png", "kdpt_hdr_encode",
     "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm", "kdpt_set_options", "kdpt_scene_build_device",
@@ -155,6 +155,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_selftest_math.argtypes = [P(C.c_float), C.c_int, P(C.c_float), P(C.c_float)]
     lib.kdpt_selftest_rng.argtypes = [P(C.c_int), C.c_int, C.c_int, P(C.c_float)]
     lib.kdpt_selftest_fresnel.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
+    lib.kdpt_selftest_rng_draws.argtypes = [C.c_int, P(C.c_uint32), C.c_int, C.c_int, P(C.c_float)]
     if hasattr(lib, "kdpt_selftest_libm"):  # absent from older builds used in A/B runs
         lib.kdpt_selftest_libm.argtypes = [C.c_int, P(C.c_float), C.c_int, P(C.c_double)]
         lib.kdpt_selftest_libm_digest.argtypes = [C.c_int, C.c_uint32, C.c_ulonglong, P(C.c_ulonglong)]

@@ -328,6 +328,16 @@ uint64_t orc_libm_digest(int fn, uint32_t first, uint64_t count) {
 void orc_u01_array(const int *iid, int n, int k, float *u) {
     for (int i = 0; i < n; i++) u[i] = orc_u01_sequence(iid[3 * i], iid[3 * i + 1], iid[3 * i + 2], k);
 }
+/* The first k draws of an engine per input, laid out n x k (the layout of oracle/ref/thrust_rng):
+   mode 0 makeSeededRandomEngine(iter, index, depth) from int triples (src/pathtrace.cu:62-66),
+   mode 1 the camera jitter's engine(utilhash(iter)) (src/pathtrace.cu:334), mode 2 engine(raw seed). */
+void orc_rng_draws(int mode, const unsigned int *in, int n, int k, float *out) {
+    for (int i = 0; i < n; i++) {
+        rng_t r = mode == 0 ? makeSeededRandomEngine((int)in[3 * i], (int)in[3 * i + 1], (int)in[3 * i + 2])
+                : mode == 1 ? rng_seed(orc_utilhash(in[i])) : rng_seed(in[i]);
+        for (int j = 0; j < k; j++) out[(size_t)i * k + j] = u01(&r);
+    }
+}
 
 /* ------------------------------------------------------------------ */
 /* Intersections (src/intersections.h)                                  */

@@ -230,6 +230,8 @@ float orc_cosf(float x);
 void orc_sincos_array(const float *x, int n, float *s, float *c);
 /* u01 draws: for each (iter, index, depth) triple, the k-th uniform of makeSeededRandomEngine */
 void orc_u01_array(const int *iid, int n, int k, float *u);
+/* first k draws per input, n x k: mode 0 seeded triples, 1 camera engine(utilhash(iter)), 2 raw seeds */
+void orc_rng_draws(int mode, const unsigned int *in, int n, int k, float *out);
 /* glibc acosf(x) (fn 0), sin((double)x) (1), cos((double)x) (2), as doubles */
 void orc_libm_array(int fn, const float *x, int n, double *out);
 /* order-independent digest of fn over the float bit patterns first .. first+count-1:

@@ -10,6 +10,12 @@ outputs on the seeded inputs of tests/kat_inputs.py --
            geom in the scene fixtures and 20 000 random translation/rotation/scale triples;
   images   image::savePNG / image::saveHDR bytes of seeded float images and of saveImage's pixels of an
            oracle render (cornell + sphere_low_1, 64x64, 4 iterations).
+  thrust_rng  the first 8 draws of thrust::default_random_engine + uniform_real_distribution<float>(0,1)
+           per seed, from rocThrust's own implementation (oracle/_ref/thrust_rng, oracle/ref/
+           thrust_rng_driver.cpp: THRUST_VERSION 200805, host-only), for makeSeededRandomEngine's
+           (iter, index, depth) grid, the camera jitter's engine(utilhash(iter)) and raw edge seeds.
+           `python tests/golden/make_ref_pins.py --thrust` refreshes only this section (it needs no
+           /root/reference).
 """
 import json
 import os
@@ -30,6 +36,7 @@ import oracle_lib  # noqa: E402
 from kdtreepathtraceroptimization_amd.fixtures import load_fixture_scene  # noqa: E402
 
 REF_PINS = os.path.join(ROOT, "oracle", "_ref", "ref_pins")
+THRUST_RNG = os.path.join(ROOT, "oracle", "_ref", "thrust_rng")
 SCENES = ("cornell", "cornell8", "cornellout_bunny")
 
 
@@ -81,7 +88,36 @@ def ref_image_files(im, tmp):
     return open(base + ".png", "rb").read(), open(base + ".hdr", "rb").read()
 
 
+def thrust_draws(mode, x, tmp, k=K.RNG_K):
+    """rocThrust's draws (n x k float32) for the inputs of kat_inputs.rng_inputs(mode)."""
+    xin, xout = os.path.join(tmp, "rng.in"), os.path.join(tmp, "rng.out")
+    x.tofile(xin)
+    n = len(x)
+    subprocess.run([THRUST_RNG, mode, str(n), xin, str(k), xout], check=True, capture_output=True)
+    return np.fromfile(xout, np.float32).reshape(n, k)
+
+
+def pin_thrust_rng(tmp):
+    out = {"source": "oracle/_ref/thrust_rng: rocThrust (THRUST_VERSION 200805) default_random_engine + "
+                     "uniform_real_distribution<float>(0, 1), host-only", "k": K.RNG_K}
+    for mode in ("seeded", "camera", "raw"):
+        x = K.rng_inputs(mode)
+        u = thrust_draws(mode, x, tmp)
+        out[mode] = {"n": len(x), "sha256": K.sha256(u), "first_row": [float(v) for v in u[0]],
+                     "min": float(u.min()), "max": float(u.max())}
+    return out
+
+
 def main():
+    if "--thrust" in sys.argv:
+        path = os.path.join(HERE, "ref_pins.json")
+        pins = json.load(open(path))
+        with tempfile.TemporaryDirectory() as tmp:
+            pins["thrust_rng"] = pin_thrust_rng(tmp)
+        with open(path, "w") as f:
+            json.dump(pins, f, indent=1)
+        print(json.dumps(pins["thrust_rng"], indent=1))
+        return
     import hashlib
     pins = {"source": "oracle/_ref/ref_pins: /root/reference src/image.cpp, src/stb.cpp, src/utilities.cpp, "
                       "external/include (glm 0.9.6.3, stb_image_write)", "glm": {}, "images": {}}
@@ -106,6 +142,7 @@ def main():
             pins["images"][name] = {"shape": list(im.shape), "png_sha256": hashlib.sha256(png).hexdigest(),
                                     "hdr_sha256": hashlib.sha256(hdr).hexdigest(), "png_len": len(png),
                                     "hdr_len": len(hdr)}
+        pins["thrust_rng"] = pin_thrust_rng(tmp)
     with open(os.path.join(HERE, "ref_pins.json"), "w") as f:
         json.dump(pins, f, indent=1)
     print(json.dumps(pins, indent=1))

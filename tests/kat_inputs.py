@@ -91,6 +91,35 @@ def images(seed: int = 3):
     return out
 
 
+RNG_K = 8  # draws per engine: scatterRay's deepest branch (fake SSS + soft lobe) draws fewer
+
+
+def rng_inputs(mode: str, seed: int = 62) -> np.ndarray:
+    """Inputs of the RNG pin (tests/golden/make_ref_pins.py, oracle/ref/thrust_rng_driver.cpp):
+    "seeded" (iter, index, depth) int32 rows for makeSeededRandomEngine (src/pathtrace.cu:62-66): the
+    grid of small iterations x every depth 0..16 x the first/last pixels of 800^2 and 1600^2, plus random
+    rows; "camera" iterations for engine(utilhash(iter)) (src/pathtrace.cu:334); "raw" uint32 seeds,
+    incl. the seeding edge cases (0, multiples of m = 2^31 - 1, m +- 1, 2^32 - 1)."""
+    rng = np.random.default_rng(seed)
+    if mode == "seeded":
+        it = np.arange(0, 33)
+        idx = np.array([0, 1, 2, 63, 64, 799, 800, 639999, 640000 - 1, 2559999, 2 ** 21, 2 ** 22 - 1])
+        d = np.arange(0, 17)
+        grid = np.stack(np.meshgrid(it, idx, d, indexing="ij"), -1).reshape(-1, 3)
+        n = 1 << 18
+        rnd = np.stack([rng.integers(1, 1 << 22, n), rng.integers(0, 1 << 22, n), rng.integers(0, 17, n)], 1)
+        return np.ascontiguousarray(np.concatenate([grid, rnd]), np.int32)
+    if mode == "camera":
+        return np.ascontiguousarray(np.concatenate([np.arange(0, 1 << 16), rng.integers(0, 1 << 31, 1 << 14)]),
+                                    np.int32)
+    if mode == "raw":
+        m = 2 ** 31 - 1
+        edge = [0, 1, 2, m - 1, m, m + 1, 2 * m - 1, 2 * m, 2 * m + 1, 2 ** 31, 2 ** 32 - 1, 48271, 16807]
+        return np.ascontiguousarray(np.concatenate([edge, rng.integers(0, 1 << 32, 1 << 16, dtype=np.uint64)]),
+                                    np.uint32)
+    raise ValueError(mode)
+
+
 def sha256(a: np.ndarray) -> str:
     return hashlib.sha256(np.ascontiguousarray(a).tobytes()).hexdigest()
 

@@ -104,6 +104,7 @@ def lib():
         L.orc_libm_digest.argtypes = [C.c_int, C.c_uint32, C.c_uint64]
         L.orc_libm_digest.restype = C.c_uint64
         L.orc_u01_array.argtypes = [P(C.c_int), C.c_int, C.c_int, P(C.c_float)]
+        L.orc_rng_draws.argtypes = [C.c_int, P(C.c_uint32), C.c_int, C.c_int, P(C.c_float)]
         L.orc_fresnel_array.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
         L.orc_trace_ray.argtypes = [P(OScene), P(C.c_float), P(C.c_float), C.c_int, P(C.c_double)]
         L.orc_save_image.argtypes = [P(C.c_float), C.c_int, C.c_int, C.c_float, P(C.c_uint8), P(C.c_float)]
@@ -280,6 +281,19 @@ def u01(iid: np.ndarray, k: int):
     u = np.empty(len(iid), np.float32)
     lib().orc_u01_array(iid.ctypes.data_as(C.POINTER(C.c_int)), len(iid), k, _fp(u))
     return u
+
+
+RNG_MODES = {"seeded": 0, "camera": 1, "raw": 2}
+
+
+def rng_draws(mode: str, x: np.ndarray, k: int):
+    """The first k uniform draws per input (n x k float32): mode "seeded" = makeSeededRandomEngine of
+    (iter, index, depth) rows, "camera" = engine(utilhash(iter)), "raw" = engine(seed)."""
+    x = np.ascontiguousarray(x, np.uint32)
+    n = len(x)
+    out = np.empty((n, k), np.float32)
+    lib().orc_rng_draws(RNG_MODES[mode], x.ctypes.data_as(C.POINTER(C.c_uint32)), n, k, _fp(out))
+    return out
 
 
 def fresnel(cosines: np.ndarray, ior: float):

@@ -10,7 +10,11 @@ src/utilities.cpp and its vendored glm 0.9.6.3, compiled in place from /root/ref
   geom and 20 000 random triples;
 - image::savePNG / image::saveHDR (src/image.cpp:22-45 over stb_image_write): the product's encoders
   give the reference's bytes for seeded images and for an oracle render; (-m gpu) kdpt_save_png /
-  kdpt_save_hdr of the GPU render of the same scene write the reference's file bytes.
+  kdpt_save_hdr of the GPU render of the same scene write the reference's file bytes;
+- the RNG (thrust::default_random_engine + uniform_real_distribution<float>, the third-party code the
+  reference draws from): the oracle, kdpt_math.h compiled for the host and (-m gpu) the gfx950 code give
+  rocThrust's own draws (oracle/_ref/thrust_rng) for makeSeededRandomEngine, the camera engine and raw
+  edge seeds.
 
 Where /root/reference exists the digests are recomputed from the reference binary as well, so the
 fixture itself stays pinned.  The bounce as a whole stays pinned only by the survey's anchor runs
@@ -192,3 +196,74 @@ def test_gpu_saved_png_hdr_equal_reference_writer(kdpt, tmp_path):
         pt.save_hdr(str(tmp_path / "r.hdr"), 4.0)
     assert hashlib.sha256((tmp_path / "r.png").read_bytes()).hexdigest() == rec["png_sha256"]
     assert hashlib.sha256((tmp_path / "r.hdr").read_bytes()).hexdigest() == rec["hdr_sha256"]
+
+
+# ---- the RNG against rocThrust's own default_random_engine + uniform_real_distribution<float> ----
+# The reference draws every random number through thrust (src/pathtrace.cu:62-66,334-335,
+# src/interactions.h:12,70,207,232,314).  ref_pins.json["thrust_rng"] holds digests of rocThrust's draws
+# (oracle/ref/thrust_rng_driver.cpp, compiled host-only against /opt/rocm/include/thrust).
+THRUST_RNG = os.path.join(ROOT, "oracle", "_ref", "thrust_rng")
+RNG_MODES = ("seeded", "camera", "raw")
+
+
+@pytest.fixture(scope="module")
+def rng_host():
+    exe = os.path.join(ROOT, "build", "rng_host")
+    os.makedirs(os.path.dirname(exe), exist_ok=True)
+    subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-I",
+                    os.path.join(ROOT, "include"), os.path.join(TESTS, "native", "rng_host.cpp"), "-o", exe],
+                   check=True)
+    return exe
+
+
+def _draws_from(exe, mode, x):
+    with tempfile.TemporaryDirectory() as tmp:
+        xin, xout = os.path.join(tmp, "in"), os.path.join(tmp, "out")
+        x.tofile(xin)
+        subprocess.run([exe, mode, str(len(x)), xin, str(K.RNG_K), xout], check=True, timeout=120)
+        return np.fromfile(xout, np.float32).reshape(len(x), K.RNG_K)
+
+
+@pytest.mark.parametrize("mode", RNG_MODES)
+def test_rng_oracle_and_host_device_source_equal_thrust(oracle, rng_host, mode):
+    x = K.rng_inputs(mode)
+    rec = PINS["thrust_rng"][mode]
+    assert len(x) == rec["n"]
+    assert K.sha256(oracle.rng_draws(mode, x, K.RNG_K)) == rec["sha256"], "oracle"
+    assert K.sha256(_draws_from(rng_host, mode, x)) == rec["sha256"], "kdpt_math.h compiled for the host"
+
+
+def test_rng_pin_inputs_cover_seeding_edges():
+    """engine(seed) maps s % m == 0 to state 1 (linear_congruential_engine::seed); the raw inputs hold
+    0, m, 2m and their neighbours, and the seeded grid holds every depth the reference's bounce cap of 16
+    reaches with the first and last pixels of 800^2 and 1600^2."""
+    raw = K.rng_inputs("raw").astype(np.int64)
+    m = 2 ** 31 - 1
+    assert {0, m, 2 * m, 2 * m + 1, 2 ** 32 - 1} <= set(raw.tolist())
+    seeded = K.rng_inputs("seeded")
+    assert set(seeded[:, 2].tolist()) == set(range(17))
+    assert {0, 639999, 2559999} <= set(seeded[:, 1].tolist())
+
+
+def test_rng_fixture_matches_thrust_binary():
+    """Rebuild rocThrust's driver (needs only hipcc and /opt/rocm/include) and recompute the digests."""
+    subprocess.run(["make", "-s", "-C", os.path.join(ROOT, "oracle", "ref"), "thrust"], check=True)
+    import make_ref_pins as M
+    with tempfile.TemporaryDirectory() as tmp:
+        for mode in RNG_MODES:
+            u = M.thrust_draws(mode, K.rng_inputs(mode), tmp)
+            assert K.sha256(u) == PINS["thrust_rng"][mode]["sha256"], mode
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", RNG_MODES)
+def test_device_rng_equals_thrust(kdpt, mode):
+    import ctypes as C
+    x = np.ascontiguousarray(K.rng_inputs(mode).view(np.uint32).reshape(-1))
+    n = len(x) // (3 if mode == "seeded" else 1)
+    out = np.empty((n, K.RNG_K), np.float32)
+    rc = kdpt.load_library().kdpt_selftest_rng_draws(
+        {"seeded": 0, "camera": 1, "raw": 2}[mode], x.ctypes.data_as(C.POINTER(C.c_uint32)), n, K.RNG_K,
+        out.ctypes.data_as(C.POINTER(C.c_float)))
+    assert rc == 0
+    assert K.sha256(out) == PINS["thrust_rng"][mode]["sha256"]

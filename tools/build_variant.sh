@@ -6,7 +6,9 @@ set -e
 NAME=$1; shift
 ROOT=$(cd "$(dirname "$0")/.." && pwd)
 mkdir -p "$ROOT/ab" "$ROOT/build/ab"
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I "$ROOT/include" "$@" \
+# the product's device code-generation flags (scheduler), so a variant differs from libkdpt.so only by "$@"
+DEVICE_FLAGS=$(cd "$ROOT" && python3 -m kdtreepathtraceroptimization_amd._build --device-flags)
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I "$ROOT/include" $DEVICE_FLAGS "$@" \
   -c "$ROOT/kdtreepathtraceroptimization_amd/csrc/kdpt_runtime.hip" -o "$ROOT/build/ab/$NAME.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/ab/$NAME.so" "$ROOT/build/ab/$NAME.o" \
   "$ROOT/build/kd_build.o" "$ROOT/build/scene_host.o" "$ROOT/build/image_io.o"

@@ -31,7 +31,8 @@ PASSES = ["pmc_sq_a", "pmc_sq_b", "pmc_fetch", "pmc_write"]
 def family(name):
     if "k_trace<" in name:
         return "k_trace" if ", false," in name else "k_trace_count"
-    for k in ("k_shade_fused", "k_shade<", "k_geoms", "k_gen_rays", "k_accumulate_batch", "k_scan", "k_scatter"):
+    for k in ("k_shade_fused", "k_shade<", "k_gen_geoms", "k_geoms", "k_gen_rays", "k_accumulate_batch", "k_scan",
+              "k_scatter"):
         if k in name:
             return k.rstrip("<")
     return "other"
@@ -142,17 +143,47 @@ def main():
             k["hbm_GBps_exclusive"] = (fb / 1e9) / (ms * 1e-3) + (wb / 1e9) / (P["pmc_write"][f]["exclusive_ms"] * 1e-3)
             k["hbm_frac_exclusive"] = k["hbm_GBps_exclusive"] / 8000.0
         out["kernels"][f] = k
-    import bench  # the kernel-source hash bench.py checks
-    out["kernel_source_sha"] = bench.kernel_source_hash()
+    # every kernel family, per dispatch (each ran alone under PMC): time, VALU issue, waits, HBM bytes
+    out["per_dispatch"] = {}
+    for f, a in P.get("pmc_sq_a", {}).items():
+        n = a["dispatches"]
+        r = {"dispatches": n, "exclusive_ms": a["exclusive_ms"] / n}
+        valu, wc = c("pmc_sq_a", f, "SQ_INSTS_VALU"), c("pmc_sq_a", f, "SQ_WAVE_CYCLES")
+        grbm = c("pmc_sq_a", f, "GRBM_GUI_ACTIVE")
+        if valu is not None:
+            r["valu_wave_insts"] = valu / n
+        if valu and grbm:
+            cus = a["cus"] / n if f == "k_trace" else 256
+            r["valu_busy_frac"] = valu * 2.0 / (grbm / 8.0 * 4 * cus)
+        if wc:
+            for name in ("SQ_WAIT_ANY", "SQ_WAIT_INST_ANY", "SQ_ACTIVE_INST_ANY"):
+                v = c("pmc_sq_b", f, name)
+                if v is not None:
+                    r[name.lower() + "_share"] = v / wc
+        fetch, write = c("pmc_fetch", f, "FETCH_SIZE"), c("pmc_write", f, "WRITE_SIZE")
+        if fetch is not None and write is not None:
+            fb, wb = 2.0 * 1024 * fetch / n, 1024 * write / n
+            r["hbm_bytes"] = fb + wb
+            fms = P["pmc_fetch"][f]["exclusive_ms"] / n
+            wms = P["pmc_write"][f]["exclusive_ms"] / n
+            r["hbm_GBps"] = fb / 1e9 / (fms * 1e-3) + wb / 1e9 / (wms * 1e-3)
+            r["hbm_frac"] = r["hbm_GBps"] / 8000.0
+        out["per_dispatch"][f] = r
+    # provenance: the bench run under PMC printed the build recipe hash and the code-object hash of the
+    # library it loaded, so the profile names the exact machine code it measured
+    roof = (b or {}).get("roofline", {})
+    out["kernel_source_sha"] = roof.get("kernel_source_sha")
+    out["code_object_sha"] = roof.get("code_object_sha")
     try:
         out["git_head"] = subprocess.run(["git", "rev-parse", "--short", "HEAD"], capture_output=True, text=True,
                                          cwd=ROOT).stdout.strip()
     except OSError:
         pass
     json.dump(out, open(dst + "_pmc.json", "w"), indent=1)
-    json.dump({"kernel_source_sha": out["kernel_source_sha"], "source": os.path.basename(dst) + "_pmc.json",
-               "kernels": out["kernels"]}, open(os.path.join(ROOT, "profiles", f"pmc_{workload}.json"), "w"), indent=1)
-    print(json.dumps(out["kernels"], indent=1))
+    json.dump({"kernel_source_sha": out["kernel_source_sha"], "code_object_sha": out["code_object_sha"],
+               "git_head": out.get("git_head"), "source": os.path.basename(dst) + "_pmc.json",
+               "kernels": out["kernels"], "per_dispatch": out["per_dispatch"]}, open(os.path.join(ROOT, "profiles", f"pmc_{workload}.json"), "w"), indent=1)
+    print(json.dumps({"kernels": out["kernels"], "per_dispatch": out["per_dispatch"]}, indent=1))
 
 
 if __name__ == "__main__":
