@@ -35,6 +35,7 @@ MESHES = {"sphere_low_1": "scenes/sphere_low_1.obj", "dragon_5": "scenes/dragon_
           # the other meshes of the reference's benchmark table (presentation/resultformat*.py) that exist
           "dragon_1": "scenes/dragon_1.obj", "dragon_2": "scenes/dragon_2.obj", "dragon_3": "scenes/dragon_3.obj",
           "dragon_4": "scenes/dragon_4.obj", "sphere_low_8": "scenes/sphere_low_8.obj",
+          **{f"sphere_low_{k}": f"scenes/sphere_low_{k}.obj" for k in range(2, 8)},
           "stanford_bunny": "scenes/stanford_bunny.obj"}
 
 

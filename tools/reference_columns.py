@@ -29,8 +29,12 @@ GTX980M = {
     "dragon_1": (53.5, 49.3, 51.7, 40.8), "dragon_2": (79.0, 72.9, 56.6, 44.0),
     "dragon_3": (156.0, 143.9, 69.1, 49.7), "dragon_4": (315.4, 294.5, 94.2, 59.0),
     "dragon_5": (642.2, 593.0, 136.4, 79.4), "sphere_low_1": (5.1, 5.2, 25.0, 25.4),
+    "sphere_low_2": (7.3, 7.1, 26.9, 27.1), "sphere_low_3": (13.1, 13.1, 27.9, 28.3),
+    "sphere_low_4": (19.1, 19.0, 28.7, 28.9), "sphere_low_5": (26.8, 26.6, 30.1, 29.7),
+    "sphere_low_6": (37.7, 36.8, 30.9, 30.4), "sphere_low_7": (49.8, 48.2, 31.6, 30.8),
     "sphere_low_8": (62.0, 60.3, 32.4, 31.3),
 }
+# presentation/resultformat_low.py:10-376 test1..test8 = sphere_low_1..8 (means of its 10 runs per column)
 MODES = {"bruteforce": dict(enable_kd=0, use_bbox=0), "bbox": dict(enable_kd=0, use_bbox=1),
          "kd": dict(enable_kd=1, short_stack=0), "short-stack": dict(enable_kd=1, short_stack=1)}
 
