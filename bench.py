@@ -20,8 +20,9 @@ bound by VALU issue and latency, not HBM (its tree lives in LDS, its triangles i
 roofline is VALU issue: peak = 256 CUs x 4 SIMDs x 1/2 wave64 VALU instruction per clock x 2.4 GHz.
 achieved = k_trace's VALU wave-instructions per launch / (launch duration x the grid share the launch ran
 on): the instructions per k_trace ray come from rocprofv3 SQ_INSTS_VALU of the same kernel sources
-(profiles/pmc_<workload>.json, matched by the hash of the kernel sources + compile flags AND the hash of
-the library's gfx950 code objects (.hip_fatbin) -- null when either differs), the rays per
+(profiles/pmc_<workload>.json, matched by the hash of the library's gfx950 code objects (.hip_fatbin),
+i.e. the exact machine code -- null when it differs; the hash of the kernel sources + compile flags is
+recorded beside it), the rays per
 launch and the launch duration are measured live (device counters, s_memrealtime).  traffic = HBM bytes
 per launch from the same profile (FETCH_SIZE x 2, the gfx950 correction of MI355X_MICROARCH.md, +
 WRITE_SIZE), scaled to the live rays per launch.
@@ -160,10 +161,13 @@ def valu_roofline(args, W, H, rays_per_launch, launch_ms, share):
         return out
     prof = json.load(open(path))
     k = prof.get("kernels", {}).get("k_trace")
-    if prof.get("kernel_source_sha") != src or prof.get("code_object_sha") != cos or not k:
-        out["note"] = (f"PMC profile is for kernel build {prof.get('kernel_source_sha')} / code object "
-                       f"{prof.get('code_object_sha')}, not {src} / {cos}: stale")
+    # the profile must have measured this exact machine code: the code objects' hash decides (the
+    # source + flags hash is recorded beside it; a comment-only source edit leaves the code objects equal)
+    if prof.get("code_object_sha") != cos or not k:
+        out["note"] = (f"PMC profile is for code object {prof.get('code_object_sha')} (kernel build "
+                       f"{prof.get('kernel_source_sha')}), not {cos} ({src}): stale")
         return out
+    out["pmc_kernel_source_sha"] = prof.get("kernel_source_sha")
     inst = k["valu_per_ray"] * rays_per_launch
     eff_s = launch_ms * 1e-3 * share  # the launch ran on `share` of the chip's CUs
     out["achieved"] = round(inst / eff_s / 1e9, 2) if eff_s > 0 else None
