@@ -201,7 +201,9 @@ int kdpt_trace_iteration_async(kdpt_ctx *ctx, int frame, int iter);
 int kdpt_synchronize(kdpt_ctx *ctx);
 /* The float3 accumulation image (sum over iterations, not averaged): 3*W*H floats. */
 int kdpt_read_image(kdpt_ctx *ctx, float *rgb);
-/* sendImageToPBO (src/pathtrace.cu:69-89) into host uchar4[W*H] (x,y,z,w bytes). */
+/* sendImageToPBO (src/pathtrace.cu:69-89) into uchar4[W*H] (x,y,z,w bytes).  `rgba` may be device memory
+ * (the reference's GL-mapped PBO: written by the kernel directly) or host memory (copied out through a
+ * staging buffer the context keeps).  Synchronous. */
 int kdpt_write_pbo(kdpt_ctx *ctx, int iter, uint8_t *rgba);
 int kdpt_reset(kdpt_ctx *ctx);
 

@@ -111,8 +111,8 @@ void pathtrace(uchar4* pbo, int frame, int iteration, float focalLength, float d
   }
   check(kdpt_trace_iteration(g_ctx, frame, iteration), "pathtrace");
   check(kdpt_read_image(g_ctx, reinterpret_cast<float*>(g_scene->state.image.data())), "pathtrace image");
-  if (pbo) {  // sendImageToPBO (src/pathtrace.cu:69-89); under CUDA-GL interop the PBO is device memory, so a
-    // GL viewer uploads these bytes with glBufferSubData -- a headless caller passes host memory directly
+  if (pbo) {  // sendImageToPBO (src/pathtrace.cu:69-89): under GL interop the PBO is the mapped device buffer,
+    // which kdpt_write_pbo writes directly; a headless caller may pass host memory instead
     check(kdpt_write_pbo(g_ctx, iteration, reinterpret_cast<uint8_t*>(pbo)), "pathtrace pbo");
   }
 }

@@ -12,6 +12,7 @@
 //        adler32; IHDR / one IDAT / IEND with CRC-32.
 //   HDR: Radiance RGBE ("32-bit_rle_rgbe"), stb's header, per-channel RLE scanlines for
 //        8 <= width < 32768, raw RGBE otherwise; RGBE from frexp of the largest component.
+// stb_image_write v0.98 (Sean Barrett) is public domain: THIRD_PARTY_NOTICES.md.
 #include <cmath>
 #include <cstdint>
 #include <cstdio>

@@ -327,6 +327,13 @@ struct Arena {
     *out = (T*)q;
     return e;
   }
+  // frees one of the arena's buffers now (the caller has synchronised every use of it)
+  hipError_t release(void* q) {
+    auto it = std::find(p.begin(), p.end(), q);
+    if (it == p.end()) return hipErrorInvalidValue;
+    p.erase(it);
+    return hipFree(q);
+  }
 };
 
 struct Scanner {
@@ -511,13 +518,18 @@ int build_kd_device(const float* v9, const float* n9, const int* mtl, int ntri, 
     const int nsplit_tot = tot[0];
     const long long npairs_next = tot[1], nleaf_tot = tot[2];
     if (nnodes + 2ll * nsplit_tot > cap || npairs_next > pcap || leaf_total + nleaf_tot > lcap) {
-      // grow and retry this level (rare: the initial capacities cover the reference meshes)
+      // grow the buffers and carry on with this level: the level's flags and scans are already in place,
+      // only the next level's outputs need the larger capacity (rare: the initial capacities cover the
+      // reference meshes).  Each replaced buffer is freed once its copy has run, so the peak device
+      // memory is the new capacity plus one old buffer, not the sum of every size.
       auto grow = [&](auto*& ptr, long long oldn, long long newn) -> hipError_t {
         using T = std::remove_reference_t<decltype(*ptr)>;
         T* q;
         hipError_t e = A.alloc(&q, (size_t)newn);
         if (e != hipSuccess) return e;
         e = hipMemcpyAsync(q, ptr, sizeof(T) * (size_t)oldn, hipMemcpyDeviceToDevice, st);
+        if (e == hipSuccess) e = hipStreamSynchronize(st);
+        if (e == hipSuccess) e = A.release(ptr);
         ptr = q;
         return e;
       };

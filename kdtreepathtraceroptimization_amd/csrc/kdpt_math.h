@@ -7,6 +7,9 @@
 // follows.  Transcendentals the reference gets from glibc are restated
 // bit-exactly (kdpt_sinf/kdpt_cosf: glibc 2.35 sysdeps/ieee754/flt-32
 // s_sinf.c/s_cosf.c FMA variant -- verified over every |x| < 119 float).
+//
+// The glibc restatements below follow GNU C Library 2.35 (LGPL-2.1-or-later; e_acosf.c also under
+// Sun Microsystems' fdlibm notice): see THIRD_PARTY_NOTICES.md at the repository root.
 #pragma once
 
 #include <stdint.h>

@@ -1594,6 +1594,7 @@ struct kdpt_ctx {
   DevScene S{};
   // owned device memory
   std::vector<void*> allocs;
+  uchar4* pbo_staging = nullptr;  // kdpt_write_pbo into host memory
   PathBuf buf[2]{};
   int cur = 0;
   float* image = nullptr;
@@ -2634,15 +2635,24 @@ int kdpt_read_image(kdpt_ctx* c, float* rgb) {
 int kdpt_write_pbo(kdpt_ctx* c, int iter, uint8_t* rgba) {
   if (!c || !rgba || iter == 0) return fail(KDPT_ERR_ARG, "bad arg");
   HIP_TRY(hipSetDevice(c->device));
-  uchar4* d = nullptr;
   int rc = join_accum(c);
   if (rc) return rc;
-  HIP_TRY(hipMalloc((void**)&d, sizeof(uchar4) * (size_t)c->npix));
+  // The reference's pbo is the GL-mapped device buffer (src/main.cpp runCuda); a headless caller passes host
+  // memory.  Device memory (of any device: peer access) is written by the kernel directly, anything else
+  // through the context's staging buffer.
+  hipPointerAttribute_t attr{};
+  const bool on_device = hipPointerGetAttributes(&attr, rgba) == hipSuccess && attr.type == hipMemoryTypeDevice;
+  (void)hipGetLastError();  // a plain host pointer is an error for hipPointerGetAttributes on some runtimes
+  uchar4* d = reinterpret_cast<uchar4*>(rgba);
+  if (!on_device) {
+    if (!c->pbo_staging) HIP_TRY(hipMalloc((void**)&c->pbo_staging, sizeof(uchar4) * (size_t)c->npix));
+    d = c->pbo_staging;
+  }
   hipLaunchKernelGGL(k_pbo, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->image, c->npix, iter, d);
   HIP_TRY(hipGetLastError());
-  HIP_TRY(hipMemcpyAsync(rgba, d, sizeof(uchar4) * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
+  if (!on_device)
+    HIP_TRY(hipMemcpyAsync(rgba, d, sizeof(uchar4) * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
-  HIP_TRY(hipFree(d));
   return KDPT_OK;
 }
 
@@ -2731,6 +2741,7 @@ int kdpt_destroy(kdpt_ctx* c) {
   if (c->accum_stream) (void)hipStreamDestroy(c->accum_stream);
   if (c->accum_ev) (void)hipEventDestroy(c->accum_ev);
   for (void* p : c->allocs) (void)hipFree(p);
+  if (c->pbo_staging) (void)hipFree(c->pbo_staging);
   if (c->h_counts) (void)hipHostFree(c->h_counts);
   if (c->ev0) (void)hipEventDestroy(c->ev0);
   if (c->ev1) (void)hipEventDestroy(c->ev1);

@@ -15,6 +15,9 @@
 // Float semantics: compiled with -ffp-contract=off, no fast-math; every float
 // and double operation is the one the reference spells (incl. its float ->
 // double promotions), libm calls go to the same glibc the reference links.
+//
+// The OBJ/MTL parsing restates tinyobjloader (MIT, Copyright (c) 2012-2016 Syoyo Fujita and many
+// contributors); its notice is in THIRD_PARTY_NOTICES.md at the repository root.
 #include <algorithm>
 #include <cfloat>
 #include <cmath>

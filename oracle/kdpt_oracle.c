@@ -4,6 +4,8 @@
  * A plain-C restatement of reddeupenn/kdtreePathTracerOptimization's
  *   - scene text parser          src/scene.cpp:7-271, src/utilities.cpp:256-303
  *   - tinyobjloader OBJ/MTL parse src/tiny_obj_loader.cpp:160-276,425-1156
+ *     (tinyobjloader is MIT, Copyright (c) 2012-2016 Syoyo Fujita and many contributors;
+ *     THIRD_PARTY_NOTICES.md)
  *   - KD build + flatten         src/KDnode.cpp:112-249, src/scene.cpp:275-968
  *   - runCuda camera             src/main.cpp:1059-1073,1111-1129
  *   - the per-sample bounce      src/pathtrace.cu:315-397 (camera rays),

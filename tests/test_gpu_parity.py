@@ -242,6 +242,23 @@ def test_pbo_matches_send_image_to_pbo(kdpt):
     assert np.array_equal(pbo[..., :3], exp.astype(np.uint8)) and (pbo[..., 3] == 0).all()
 
 
+def test_pbo_into_device_memory(kdpt):
+    """The reference's pbo is the GL-mapped device buffer: kdpt_write_pbo writes device memory directly (the
+    drop-in shim passes it through) and gives the same bytes as the host-memory form."""
+    import ctypes as C
+    import torch
+    desc = load_fixture_scene("cornell", "sphere_low_1", res=(32, 24), depth=8)
+    with _pt(kdpt, desc) as pt:
+        for it in (1, 2):
+            pt.trace_iteration(it)
+        host = pt.pbo(2)
+        dev = torch.full((24, 32, 4), 7, dtype=torch.uint8, device="cuda:0")
+        torch.cuda.synchronize()
+        rc = pt.lib.kdpt_write_pbo(pt._ctx, 2, C.cast(C.c_void_p(dev.data_ptr()), C.POINTER(C.c_uint8)))
+        assert rc == 0
+        assert np.array_equal(dev.cpu().numpy(), host)
+
+
 @pytest.mark.parametrize("pipeline,batch", [(1, 1), (3, 1), (2, 3), (1, 4), (8, 4), (5, 2)])
 def test_pipelined_iterations_bit_exact(kdpt, pipeline, batch):
     """kdpt_trace_iterations (batches sharing intersect launches, several batches in flight, partial

@@ -83,11 +83,26 @@ def _synthetic(seed, n):
     return v, nrm
 
 
+def _growth_soup(nbig=200, nsmall=200, seed=5):
+    """Triangles spanning the whole box (listed on both sides of every split) mixed with small ones: the
+    (node, triangle) pairs outgrow the initial 3 x ntri capacity after three levels, so the level loop grows
+    its buffers mid-build (kd_build.hip, `grow`)."""
+    rng = np.random.default_rng(seed)
+    big = np.tile(np.array([-1, -1, -1, 1, 1, 1, 1, -1, 1], np.float32), (nbig, 1))
+    big += rng.uniform(-0.01, 0.01, big.shape).astype(np.float32)
+    c = rng.uniform(-0.9, 0.9, (nsmall, 1, 3))
+    small = (c + rng.uniform(-0.02, 0.02, (nsmall, 3, 3))).reshape(nsmall, 9).astype(np.float32)
+    v = np.concatenate([big, small])[rng.permutation(nbig + nsmall)]
+    return np.ascontiguousarray(v), rng.normal(size=v.shape).astype(np.float32)
+
+
 @pytest.mark.gpu
 @pytest.mark.parametrize("case", ["one", "two", "three", "identical", "signed_zero_root", "random_500",
-                                  "random_20000"])
+                                  "random_20000", "growth"])
 def test_synthetic_soups_byte_identical(kdpt, case):
-    if case.startswith("random"):
+    if case == "growth":
+        v, n = _growth_soup()
+    elif case.startswith("random"):
         v, n = _synthetic(int(case.split("_")[1]), int(case.split("_")[1]))
     else:
         base = np.array([[0, 1, 0, 1, 1, 0, 0, 2, 0]], np.float32)
