@@ -305,6 +305,7 @@ def main():
                    "scene": args.scene, "mesh": args.mesh, "resolution": [W, H], "depth": args.depth,
                    "bounce_cap": args.bounce_cap, "spp_per_step": S,
                    "kd_nodes": sd.view.num_nodes, "kd_tri_refs": sd.view.num_tris,
+                   "intersect": pt.trace_config(),
                    **({"tuning": args.tune} if args.tune else {}),
                    "parallelism": (f"spp-sharded x{world} + " + ("RCCL reduce" if args.dist_backend == "nccl" else
                                                                  "gloo host reduce (ranks sharing GPUs)"))

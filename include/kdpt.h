@@ -236,6 +236,10 @@ int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
  * 0 = camera rays and bounce 0's k_geoms as two launches instead of one k_gen_geoms_b),
  * "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots (they are remade). */
 int kdpt_set_tuning(kdpt_ctx *ctx, const char *name, double value);
+/* The intersect kernel's configuration: tree source (0 HBM 64-byte records, 1 HBM 32-byte, 2 LDS 32-byte,
+ * 3 LDS 16-byte derived-box records + cluster boxes, 4 LDS 16-byte records with cluster boxes in HBM),
+ * workgroup size, persistent grid (workgroups of the full grid) and dynamic LDS bytes per workgroup. */
+int kdpt_trace_config(kdpt_ctx *ctx, int *tree_mode, int *block, int *grid, long long *lds_bytes);
 int kdpt_destroy(kdpt_ctx *ctx);
 const char *kdpt_last_error(void);
 

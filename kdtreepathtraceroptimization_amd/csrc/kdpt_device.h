@@ -94,6 +94,7 @@ struct DevScene {
   // that no float move can canonicalise the -1 links
   const int4* nodes;
   const int4* pnodes;  // the same tree as 32-byte NodesPacked records, or null when ineligible
+  const int4* dnodes;  // ... and as 16-byte NodesDerived records (boxes derived on the walk), or null
   // triangles: v0 (w = mtlIdx bits), e1 = v1-v0, e2 = v2-v0 (exactly glm's e1/e2)
   const float4* tv0;
   const float4* te1;
@@ -445,10 +446,16 @@ struct NodeRec {
   bool hasL, hasR;
   uint32_t has;  // hasL | hasR << 1
   bool tris;     // triSize > 0
+  // NodesDerived only: the value both children write into their copy of this box (the centre along
+  // `axis`), the value of the box coordinate this node changed in its parent's box, and that coordinate's
+  // slot kc (0-2 min.xyz, 3-5 max.xyz; 7 for the root)
+  float center, restore;
+  uint32_t kc;
 };
 
 struct NodesWide {
   static constexpr bool kLeafHoldsCluster = false;  // big leaves: clusters from DevScene::leaf_cl
+  static constexpr bool kDerivedBox = false;        // the record holds the node's box
   const int4* p;
   __device__ NodeRec operator()(int i) const {
     const int4 q0 = p[4 * i], q1 = p[4 * i + 1], q2 = p[4 * i + 2];
@@ -473,6 +480,7 @@ __device__ inline int link16(uint32_t v) { return v == 0xffffu ? -1 : (int)v; }
 
 struct NodesPacked {
   static constexpr bool kLeafHoldsCluster = true;  // big leaves: triStart holds the first cluster
+  static constexpr bool kDerivedBox = false;
   const int4* p;  // global or LDS (address space inferred after inlining)
   __device__ NodeRec operator()(int i) const {
     // two 16-byte vector loads (as int4 fields the compiler reads the record in four pieces)
@@ -493,6 +501,45 @@ struct NodesPacked {
     r.axis = (int)((w7 >> 16) & 3u);
     r.triStart = (int)w6;
     r.triSize = tris ? (int)(w7 >> 19) : 0;
+    return r;
+  }
+};
+
+// NodesDerived: 16-byte records (LDS), half of NodesPacked, so that two intersect workgroups share a CU and
+// the C5 icosphere's tree fits in LDS.  The reference's builder gives every child its parent's box with ONE
+// coordinate replaced by the parent's centre along the parent's axis (src/KDnode.cpp:209-213,235-239: max
+// for the left child, min for the right), and the traversal only ever moves parent <-> child, so a lane
+// keeps the current node's box in registers and updates that one coordinate per move -- the same float
+// bits the record would have held (kdpt_create checks the derivation on every node, else no NodesDerived).
+//     w0 = restore: the parent's value of the coordinate this node replaced (climbing puts it back)
+//     w1 = centre along axis (the value a descent writes), or the first triangle / cluster of a leaf
+//     w2 = left | right << 16 (0xffff = -1), or triSize of a leaf with triangles
+//     w3 = parent (16 bits) | axis << 16 | hasTris << 18 | hasLeft << 19 | hasRight << 20 | kc << 21
+struct NodesDerived {
+  static constexpr bool kLeafHoldsCluster = true;
+  static constexpr bool kDerivedBox = true;
+  const int4* p;
+  __device__ NodeRec operator()(int i) const {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const v4i q = reinterpret_cast<const v4i*>(p)[i];  // one 16-byte load
+    const uint32_t w2 = (uint32_t)q.z, w3 = (uint32_t)q.w;
+    const bool tris = (w3 >> 18) & 1u;
+    NodeRec r;
+    r.b0 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+    r.b1 = r.b0;
+    r.restore = ibits(q.x);
+    r.center = ibits(q.y);
+    r.triStart = q.y;
+    r.left = (int)(w2 & 0xffffu);  // raw: only read when hasL / hasR
+    r.right = (int)(w2 >> 16);
+    r.triSize = tris ? (int)w2 : 0;
+    r.has = tris ? 0u : (w3 >> 19) & 3u;
+    r.hasL = (r.has & 1u) != 0u;
+    r.hasR = (r.has & 2u) != 0u;
+    r.tris = tris;
+    r.parent = link16(w3 & 0xffffu);
+    r.axis = (int)((w3 >> 16) & 3u);
+    r.kc = (w3 >> 21) & 7u;
     return r;
   }
 };
@@ -697,7 +744,18 @@ struct WaveRay {
   int guard;
   Hit h;
   int objTri;  // the triangle whose hit record won (valid when h.obj_intersect)
+  float lx, ly, lz, hx, hy, hz;  // NodesDerived: the box of node cur (min.xyz, max.xyz)
 };
+
+// Replace box slot k (0-2 min.xyz, 3-5 max.xyz; anything else: none) by v.
+__device__ __attribute__((always_inline)) inline void box_set(WaveRay& R, uint32_t k, float v) {
+  R.lx = k == 0u ? v : R.lx;
+  R.ly = k == 1u ? v : R.ly;
+  R.lz = k == 2u ? v : R.lz;
+  R.hx = k == 3u ? v : R.hx;
+  R.hy = k == 4u ? v : R.hy;
+  R.hz = k == 5u ? v : R.hz;
+}
 
 // Start a ray: t_min / hit_geom_index come from the analytic geoms (k_geoms), tested first as in
 // pathTraceOneBounceKDbare.
@@ -720,6 +778,12 @@ __device__ inline void wave_ray_start(const DevScene& S, WaveRay& R, f3 o, f3 d,
   R.h.ip = mk3(0, 0, 0);
   R.h.normal = mk3(0, 0, 0);
   R.objTri = -1;
+  R.lx = S.rlo.x;  // the root's box (NodesDerived)
+  R.ly = S.rlo.y;
+  R.lz = S.rlo.z;
+  R.hx = S.rhi.x;
+  R.hy = S.rhi.y;
+  R.hz = S.rhi.z;
   W->od[lane] = make_float4(o.x, o.y, o.z, d.x);
   W->dd[lane] = make_float2(d.y, d.z);
 }
@@ -784,9 +848,11 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     const uint32_t vb = (2u * Lu - 2u + ((ps >> ((Lu - 1u) & 31u)) & 1u)) & 31u;  // own flag (L > 0)
     const bool curVis = (L == 0) ? ((fl & F_ROOTV) != 0u) : (((cb >> vb) & 1u) != 0u);
     const bool isRoot = cur == S.root;
+    const float4 nb0 = NodeSrc::kDerivedBox ? make_float4(R.lx, R.ly, R.lz, R.hx) : nd.b0;
+    const float4 nb1 = NodeSrc::kDerivedBox ? make_float4(R.hy, R.hz, 0.0f, 0.0f) : nd.b1;
     float dd;
-    const bool hg = fastAABB ? intersectAABB_fast(o, invdir, nd.b0, nd.b1, dd)
-                             : intersectAABB(o, invdir, nd.b0, nd.b1, dd);
+    const bool hg = fastAABB ? intersectAABB_fast(o, invdir, nb0, nb1, dd)
+                             : intersectAABB(o, invdir, nb0, nb1, dd);
     const bool up = curVis || !hg || dd > bz;
     // Child choice on bit masks: `has` = children present (bit 0 left, bit 1 right), `avail` = present and not
     // yet visited at this level; the near side (fside: 0 left, 1 right) is taken when available, else the far
@@ -827,6 +893,12 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       L += descend ? 1 : (climb ? -1 : 0);
       guard++;
       fl = nfl;
+      if (NodeSrc::kDerivedBox) {
+        // descending: the child's box is this one with max[axis] (left child) / min[axis] (right) set to the
+        // centre; climbing: the parent's box is this one with the coordinate this node replaced put back
+        const uint32_t kd = (nside ? 0u : 3u) + (uint32_t)nd.axis;
+        box_set(R, descend ? kd : (climb ? nd.kc : 7u), descend ? nd.center : nd.restore);
+      }
     }
   }
   rootv = (fl & F_ROOTV) != 0u;
@@ -847,11 +919,17 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   // a leaf neither climbs nor descends, so cur is the leaf)
   const int lnode = cur;
   int lstart = 0, lsize = 0, lparent = -1;
+  uint32_t lkc = 7u;
+  float lrestore = 0.0f;
   if (leaf) {
     const NodeRec ln = nodes(cur);
     lstart = ln.triStart;
     lsize = ln.triSize;
     lparent = ln.parent;
+    if (NodeSrc::kDerivedBox) {
+      lkc = ln.kc;
+      lrestore = ln.restore;
+    }
   }
   // ---------------- leaf phase (wave-cooperative) ----------------
   // per lane results of this phase
@@ -1064,6 +1142,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     done = cur == S.root;
     cur = lparent;
     L--;
+    if (NodeSrc::kDerivedBox) box_set(R, lkc, lrestore);  // back to the parent's box
   }
   if (COUNT) prof_lap(WP, PROF_FINAL_CYC);
 }

@@ -171,7 +171,10 @@ struct GenIter {
 // and objMaterialIdx; k_shade recomputes the winner's point and normal with the
 // same functions, so nothing else needs to travel.
 // ---------------------------------------------------------------------------
-enum TreeMode { TREE_WIDE = 0, TREE_PACKED = 1, TREE_LDS = 2 };
+// TREE_LDS: 32-byte NodesPacked records in LDS (+ the cluster boxes); TREE_LDS16: 16-byte NodesDerived
+// records + cluster boxes in LDS; TREE_LDS16G: NodesDerived in LDS, cluster boxes in HBM/L2 (trees whose
+// clusters do not fit, e.g. the C5 icosphere: 2 655 nodes = 41 KB, 22 848 clusters = 714 KB)
+enum TreeMode { TREE_WIDE = 0, TREE_PACKED = 1, TREE_LDS = 2, TREE_LDS16 = 3, TREE_LDS16G = 4 };
 #ifndef KDPT_TRACE_BLOCK
 #define KDPT_TRACE_BLOCK 1024  // tools/build_variant.sh experiments only
 #endif
@@ -181,8 +184,16 @@ constexpr int TRACE_BLOCK = KDPT_TRACE_BLOCK;  // LDS mode: one workgroup per CU
 #endif
 // workgroup size of the intersect kernel: with the tree in LDS every wave of a CU must share the copy,
 // otherwise small workgroups let the tail of one launch hold only a quarter of a CU
+// NodesDerived halves the tree copy.  Two 512-thread workgroups per CU (30 KB of per-wave leaf scratch + 46 KB
+// of tree and cluster boxes each for dragon_5), so that one workgroup's launch tail would overlap the next
+// one's start, measured 5.5 % slower than one 1024-thread workgroup (profiles/r03_ab_log.md)
+#ifndef KDPT_TRACE_BLOCK16
+#define KDPT_TRACE_BLOCK16 1024  // tools/build_variant.sh experiments only
+#endif
+constexpr int TRACE_BLOCK16 = KDPT_TRACE_BLOCK16;
+constexpr bool tree_in_lds(int mode) { return mode >= 2; }
 template <int MODE>
-constexpr int trace_block() { return MODE == 2 ? TRACE_BLOCK : 256; }
+constexpr int trace_block() { return MODE == 2 ? TRACE_BLOCK : (MODE >= 3 ? TRACE_BLOCK16 : 256); }
 
 // Up to MAXB iterations (each its own path buffers) at the same bounce share one intersect launch:
 // more rays per launch keep the lanes of the persistent waves busy.
@@ -455,7 +466,7 @@ __device__ unsigned long long g_tail_prof[4];
 #endif
 // (only with the tree in LDS: the 256-thread workgroups of the other modes share CUs anyway, and the C5
 // icosphere, whose tree lives in HBM, lost 3.5 % to the cap)
-#define KDPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(MODE == TREE_LDS ? KDPT_TRACE_WAVES : 1)))
+#define KDPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(tree_in_lds(MODE) ? KDPT_TRACE_WAVES : 1)))
 template <bool HYBRID, bool COUNT, int MODE>
 __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(TraceArgs A) {
   constexpr int TB = trace_block<MODE>();
@@ -468,14 +479,19 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
 #pragma unroll
   for (int b = 0; b < MAXB; b++) pre[b + 1] = pre[b] + (b < A.nb ? A.it[b].ccount[A.depth] : 0);
   const int n = pre[MAXB];
-  if (MODE == TREE_LDS) {
+  // tree copy: NodesPacked (2 x 16 bytes per node) or NodesDerived (16 bytes), then the cluster boxes
+  constexpr int NODE_WORDS = MODE == TREE_LDS ? 2 : 1;
+  if (tree_in_lds(MODE)) {
     if (n == 0) return;  // uniform: nothing to trace
-    const int words = 2 * S.num_nodes;
-    for (int k = threadIdx.x; k < words; k += TB) s_tree[k] = S.pnodes[k];
-    float4* s_cl = reinterpret_cast<float4*>(s_tree + words);
-    for (int k = threadIdx.x; k < S.num_clusters; k += TB) {
-      s_cl[2 * k] = S.cl_lo[k];
-      s_cl[2 * k + 1] = S.cl_hi[k];
+    const int words = NODE_WORDS * S.num_nodes;
+    const int4* src = MODE == TREE_LDS ? S.pnodes : S.dnodes;
+    for (int k = threadIdx.x; k < words; k += TB) s_tree[k] = src[k];
+    if (MODE != TREE_LDS16G) {
+      float4* s_cl = reinterpret_cast<float4*>(s_tree + words);
+      for (int k = threadIdx.x; k < S.num_clusters; k += TB) {
+        s_cl[2 * k] = S.cl_lo[k];
+        s_cl[2 * k + 1] = S.cl_hi[k];
+      }
     }
     __syncthreads();
   }
@@ -582,6 +598,13 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
         trace_phase<HYBRID, COUNT>(S, NodesPacked{s_tree},
                                    ClustersInterleaved{reinterpret_cast<const float4*>(s_tree + 2 * S.num_nodes)}, R,
                                    fastAABB, S.num_materials, cnt, W, P);
+      else if (MODE == TREE_LDS16)
+        trace_phase<HYBRID, COUNT>(S, NodesDerived{s_tree},
+                                   ClustersInterleaved{reinterpret_cast<const float4*>(s_tree + S.num_nodes)}, R,
+                                   fastAABB, S.num_materials, cnt, W, P);
+      else if (MODE == TREE_LDS16G)
+        trace_phase<HYBRID, COUNT>(S, NodesDerived{s_tree}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
+                                   S.num_materials, cnt, W, P);
       else if (MODE == TREE_PACKED)
         trace_phase<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
                                    S.num_materials, cnt, W, P);
@@ -1615,6 +1638,7 @@ struct kdpt_ctx {
   int full_trace_grid = 0;  // the occupancy-derived grid (trace_grid before a "trace_grid_frac" knob)
   bool grid_env = false;  // trace_grid fixed by the "trace_grid_frac" tuning knob
   bool force_global_tree = false;  // "tree_global" tuning knob: keep the tree in HBM/L2
+  int tree_format = 0;             // "tree_format" knob: 16 / 32 = LDS node records of that size only
   size_t tree_lds = 0;    // dynamic LDS bytes of the intersect kernel (TREE_LDS)
   int* tile_counts = nullptr;
   int* tile_off = nullptr;
@@ -1948,6 +1972,54 @@ bool pack_nodes(const kdpt_node_bare* N, int nn, const std::vector<int2>& leaf_c
   return true;
 }
 
+// NodesDerived records (kdpt_device.h); false unless every node's box is its parent's with exactly the one
+// coordinate the reference's split replaces (checked bit for bit), both children write the same centre, and
+// the tree fits the 16-bit links.
+bool pack_nodes16(const kdpt_node_bare* N, int nn, const std::vector<int2>& leaf_cl, std::vector<int4>& out) {
+  if (nn < 1 || nn >= 0xffff || N[0].parentID != -1) return false;
+  out.assign((size_t)nn, make_int4(0, 0, 0, 0));
+  auto l16 = [](int v) { return v == -1 ? 0xffffu : (uint32_t)v; };
+  auto same = [](float a, float b) { return fbits(a) == fbits(b); };
+  for (int i = 0; i < nn; i++) {
+    const kdpt_node_bare& n = N[i];
+    const bool tris = n.triIdSize > 0;
+    if (tris && (n.leftID != -1 || n.rightID != -1)) return false;
+    if (n.axis < 0 || n.axis > 2) return false;
+    for (int ch : {n.leftID, n.rightID})
+      if (ch != -1 && (ch <= 0 || ch >= nn || N[ch].parentID != i)) return false;
+    uint32_t kc = 7u;
+    float restore = 0.0f;
+    if (i > 0) {
+      const int p = n.parentID;
+      if (p < 0 || p >= nn) return false;
+      const kdpt_node_bare& P = N[p];
+      const bool isL = P.leftID == i, isR = P.rightID == i;
+      if (isL == isR) return false;
+      const int a = P.axis;
+      for (int k = 0; k < 3; k++) {
+        if (!(k == a && isR) && !same(n.mins[k], P.mins[k])) return false;
+        if (!(k == a && isL) && !same(n.maxs[k], P.maxs[k])) return false;
+      }
+      kc = isR ? (uint32_t)a : 3u + (uint32_t)a;
+      restore = isR ? P.mins[a] : P.maxs[a];
+    }
+    float center = 0.0f;
+    if (n.leftID != -1) center = N[n.leftID].maxs[n.axis];
+    if (n.rightID != -1) {
+      if (n.leftID != -1 && !same(center, N[n.rightID].mins[n.axis])) return false;
+      center = N[n.rightID].mins[n.axis];
+    }
+    const uint32_t first = n.triIdSize >= BIG_LEAF ? (uint32_t)leaf_cl[i].x : (uint32_t)n.triIdStart;
+    const uint32_t w1 = tris ? first : fbits(center);
+    const uint32_t w2 = tris ? (uint32_t)n.triIdSize : (l16(n.leftID) | (l16(n.rightID) << 16));
+    const uint32_t kids = (n.leftID != -1 ? 1u : 0u) | (n.rightID != -1 ? 2u : 0u);
+    const uint32_t w3 = l16(n.parentID) | ((uint32_t)n.axis << 16) | ((tris ? 1u : 0u) << 18) |
+                        ((tris ? 0u : kids) << 19) | (kc << 21);
+    out[i] = make_int4(fbits(restore), (int)w1, (int)w2, (int)w3);
+  }
+  return true;
+}
+
 template <bool HYBRID, bool COUNT, int MODE>
 int trace_occupancy(kdpt_ctx* c, size_t lds, int* blocks) {
   if (lds > 0)
@@ -1957,43 +2029,67 @@ int trace_occupancy(kdpt_ctx* c, size_t lds, int* blocks) {
   return KDPT_OK;
 }
 
-// Pick where the intersect kernel reads the tree from, and its persistent grid.
-int setup_trace(kdpt_ctx* c) {
-  hipDeviceProp_t prop;
-  HIP_TRY(hipGetDeviceProperties(&prop, c->device));
-  c->tree_mode = c->S.pnodes ? TREE_PACKED : TREE_WIDE;
-  c->tree_lds = 0;
-  // (the counting kernel's per-wave WaveProf too: the tree must fit next to either kernel's static part)
-  const size_t static_lds = (sizeof(WaveLeafLDS) + sizeof(WaveProf)) * (TRACE_BLOCK / 64);
-  const size_t tree_bytes = 32 * (size_t)c->S.num_nodes + 32 * (size_t)c->S.num_clusters;  // + cluster boxes
-  const size_t lds_max = prop.sharedMemPerBlock > 0 ? prop.sharedMemPerBlock : 65536;
-  if (c->S.pnodes && static_lds + tree_bytes <= lds_max && !c->force_global_tree) {
-    c->tree_mode = TREE_LDS;
-    c->tree_lds = tree_bytes;
-  }
-  int blocks = 0;
-  int rc = KDPT_OK;
+template <int MODE>
+int trace_occupancy_all(kdpt_ctx* c, size_t lds, int* blocks) {
+  int best = 0, rc = KDPT_OK;
   for (int hyb = 0; hyb < 2 && !rc; hyb++)
     for (int cnt = 0; cnt < 2 && !rc; cnt++) {
       int b = 0;
-      if (c->tree_mode == TREE_LDS)
-        rc = hyb ? (cnt ? trace_occupancy<true, true, TREE_LDS>(c, c->tree_lds, &b)
-                        : trace_occupancy<true, false, TREE_LDS>(c, c->tree_lds, &b))
-                 : (cnt ? trace_occupancy<false, true, TREE_LDS>(c, c->tree_lds, &b)
-                        : trace_occupancy<false, false, TREE_LDS>(c, c->tree_lds, &b));
-      else if (c->tree_mode == TREE_PACKED)
-        rc = hyb ? (cnt ? trace_occupancy<true, true, TREE_PACKED>(c, 0, &b)
-                        : trace_occupancy<true, false, TREE_PACKED>(c, 0, &b))
-                 : (cnt ? trace_occupancy<false, true, TREE_PACKED>(c, 0, &b)
-                        : trace_occupancy<false, false, TREE_PACKED>(c, 0, &b));
-      else
-        rc = hyb ? (cnt ? trace_occupancy<true, true, TREE_WIDE>(c, 0, &b)
-                        : trace_occupancy<true, false, TREE_WIDE>(c, 0, &b))
-                 : (cnt ? trace_occupancy<false, true, TREE_WIDE>(c, 0, &b)
-                        : trace_occupancy<false, false, TREE_WIDE>(c, 0, &b));
-      if (!rc && (blocks == 0 || b < blocks)) blocks = b;
+      rc = hyb ? (cnt ? trace_occupancy<true, true, MODE>(c, lds, &b) : trace_occupancy<true, false, MODE>(c, lds, &b))
+               : (cnt ? trace_occupancy<false, true, MODE>(c, lds, &b) : trace_occupancy<false, false, MODE>(c, lds, &b));
+      if (!rc && (best == 0 || b < best)) best = b;
     }
-  if (rc) return rc;
+  *blocks = best;
+  return rc;
+}
+
+// Pick where the intersect kernel reads the tree from, and its persistent grid: in LDS when it fits (the
+// "tree_format" knob limits the LDS records to one size) -- the candidate that keeps the most intersect waves
+// on a CU wins, ties in the order below.
+int setup_trace(kdpt_ctx* c) {
+  hipDeviceProp_t prop;
+  HIP_TRY(hipGetDeviceProperties(&prop, c->device));
+  const size_t lds_max = prop.sharedMemPerBlock > 0 ? prop.sharedMemPerBlock : 65536;
+  // (the counting kernel's per-wave WaveProf too: the tree must fit next to either kernel's static part)
+  const size_t per_wave = sizeof(WaveLeafLDS) + sizeof(WaveProf);
+  const size_t cl_bytes = 32 * (size_t)c->S.num_clusters;
+  struct Cand { int mode; size_t lds; };
+  std::vector<Cand> cands;
+  // (in order of preference at equal occupancy: the 32-byte records need no box bookkeeping on the walk, which
+  // costs the derived form 6 % on dragon_5; the derived form is what fits the C5 icosphere's tree)
+  if (!c->force_global_tree) {
+    if (c->S.pnodes && c->tree_format != 16) {
+      const size_t t32 = 32 * (size_t)c->S.num_nodes + cl_bytes, st32 = per_wave * (TRACE_BLOCK / 64);
+      if (st32 + t32 <= lds_max) cands.push_back({TREE_LDS, t32});
+    }
+    if (c->S.dnodes && c->tree_format != 32) {
+      const size_t t16 = 16 * (size_t)c->S.num_nodes, st16 = per_wave * (TRACE_BLOCK16 / 64);
+      if (st16 + t16 + cl_bytes <= lds_max) cands.push_back({TREE_LDS16, t16 + cl_bytes});
+      if (st16 + t16 <= lds_max) cands.push_back({TREE_LDS16G, t16});
+    }
+  }
+  c->tree_mode = c->S.pnodes ? TREE_PACKED : TREE_WIDE;
+  c->tree_lds = 0;
+  int blocks = 0, best_waves = 0, rc = KDPT_OK;
+  for (const Cand& k : cands) {
+    int b = 0;
+    rc = k.mode == TREE_LDS16 ? trace_occupancy_all<TREE_LDS16>(c, k.lds, &b)
+       : k.mode == TREE_LDS16G ? trace_occupancy_all<TREE_LDS16G>(c, k.lds, &b)
+                                : trace_occupancy_all<TREE_LDS>(c, k.lds, &b);
+    if (rc) return rc;
+    const int waves = b * (k.mode == TREE_LDS ? TRACE_BLOCK : TRACE_BLOCK16) / 64;
+    if (b > 0 && waves > best_waves) {
+      best_waves = waves;
+      blocks = b;
+      c->tree_mode = k.mode;
+      c->tree_lds = k.lds;
+    }
+  }
+  if (c->tree_lds == 0) {
+    rc = c->tree_mode == TREE_PACKED ? trace_occupancy_all<TREE_PACKED>(c, 0, &blocks)
+                                     : trace_occupancy_all<TREE_WIDE>(c, 0, &blocks);
+    if (rc) return rc;
+  }
   if (blocks < 1) return fail(KDPT_ERR_UNSUPPORTED, "intersect kernel does not fit on a CU");
   c->trace_grid = blocks * prop.multiProcessorCount;
   c->full_trace_grid = c->trace_grid;
@@ -2258,6 +2354,12 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
       if ((rc = dupload(c, &dp, packed.data(), packed.size()))) return bail(rc);
       c->S.pnodes = dp;
     }
+    c->S.dnodes = nullptr;
+    if (pack_nodes16(sc->nodes, nn, leaf_cl, packed)) {
+      int4* dp;
+      if ((rc = dupload(c, &dp, packed.data(), packed.size()))) return bail(rc);
+      c->S.dnodes = dp;
+    }
     c->S.tv0 = dtv;
     c->S.te1 = de1;
     c->S.te2 = de2;
@@ -2445,8 +2547,13 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     if (!(value > 0.0 && value <= 1.0)) return fail(KDPT_ERR_ARG, "trace_grid_frac must be in (0, 1]");
     c->trace_grid = std::max(1, (int)(c->full_trace_grid * value));
     c->grid_env = value < 1.0;
-  } else if (k == "tree_global") {
-    c->force_global_tree = v != 0;
+  } else if (k == "tree_format" || k == "tree_global") {
+    if (k == "tree_format") {
+      if (v != 0 && v != 16 && v != 32) return fail(KDPT_ERR_ARG, "tree_format must be 0 (best), 16 or 32");
+      c->tree_format = v;
+    } else {
+      c->force_global_tree = v != 0;
+    }
     const double frac = (double)c->trace_grid / std::max(1, c->full_trace_grid);
     int rc = setup_trace(c);
     if (rc) return rc;
@@ -2629,6 +2736,17 @@ int kdpt_read_image(kdpt_ctx* c, float* rgb) {
   if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
   HIP_TRY(hipMemcpyAsync(rgb, c->image, sizeof(float) * 3 * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
+  return KDPT_OK;
+}
+
+int kdpt_trace_config(kdpt_ctx* c, int* tree_mode, int* block, int* grid, long long* lds_bytes) {
+  if (!c) return fail(KDPT_ERR_ARG, "null ctx");
+  const int m = c->tree_mode;
+  if (tree_mode) *tree_mode = m;
+  if (block)
+    *block = m == TREE_LDS ? trace_block<TREE_LDS>() : (m >= TREE_LDS16 ? trace_block<TREE_LDS16>() : trace_block<TREE_PACKED>());
+  if (grid) *grid = c->full_trace_grid;
+  if (lds_bytes) *lds_bytes = (long long)c->tree_lds;
   return KDPT_OK;
 }
 
@@ -2956,13 +3074,17 @@ namespace {
 
 template <bool HYBRID, bool COUNT>
 void launch_trace_mode(kdpt_ctx* c, const TraceArgs& a, hipStream_t st) {
-  const dim3 g(c->trace_grid), b(c->tree_mode == TREE_LDS ? trace_block<TREE_LDS>() : trace_block<TREE_PACKED>());
+  const dim3 g(c->trace_grid);
   if (c->tree_mode == TREE_LDS)
-    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS>), g, b, c->tree_lds, st, a);
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS>), g, dim3(trace_block<TREE_LDS>()), c->tree_lds, st, a);
+  else if (c->tree_mode == TREE_LDS16)
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS16>), g, dim3(trace_block<TREE_LDS16>()), c->tree_lds, st, a);
+  else if (c->tree_mode == TREE_LDS16G)
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS16G>), g, dim3(trace_block<TREE_LDS16G>()), c->tree_lds, st, a);
   else if (c->tree_mode == TREE_PACKED)
-    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_PACKED>), g, b, 0, st, a);
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_PACKED>), g, dim3(trace_block<TREE_PACKED>()), 0, st, a);
   else
-    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_WIDE>), g, b, 0, st, a);
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_WIDE>), g, dim3(trace_block<TREE_WIDE>()), 0, st, a);
 }
 
 void launch_trace(kdpt_ctx* c, const TraceArgs& a, bool count, hipStream_t st) {

@@ -113,7 +113,7 @@ EXPORTS = [
     "kdpt_selftest_fresnel", "kdpt_selftest_libm", "kdpt_selftest_libm_digest", "kdpt_scene_load", "kdpt_scene_build", "kdpt_scene_view", "kdpt_scene_free",
     "kdpt_save_rgb8", "kdpt_save_png", "kdpt_save_hdr", "kdpt_png_encode", "kdpt_write_png", "kdpt_hdr_encode",
     "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm", "kdpt_set_options", "kdpt_scene_build_device",
-    "kdpt_scene_kd_build_ms", "kdpt_build_kd_device", "kdpt_scene_load_device",
+    "kdpt_scene_kd_build_ms", "kdpt_build_kd_device", "kdpt_scene_load_device", "kdpt_trace_config",
 ]
 
 _lib = None
@@ -155,6 +155,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_selftest_math.argtypes = [P(C.c_float), C.c_int, P(C.c_float), P(C.c_float)]
     lib.kdpt_selftest_rng.argtypes = [P(C.c_int), C.c_int, C.c_int, P(C.c_float)]
     lib.kdpt_selftest_fresnel.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
+    lib.kdpt_trace_config.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int), P(C.c_longlong)]
     lib.kdpt_selftest_rng_draws.argtypes = [C.c_int, P(C.c_uint32), C.c_int, C.c_int, P(C.c_float)]
     if hasattr(lib, "kdpt_selftest_libm"):  # absent from older builds used in A/B runs
         lib.kdpt_selftest_libm.argtypes = [C.c_int, P(C.c_float), C.c_int, P(C.c_double)]
@@ -467,6 +468,16 @@ class PathTracer:
         out = (C.c_ulonglong * 3)()
         _check(self.lib.kdpt_count_iteration(self._ctx, int(iteration), out), "kdpt_count_iteration")
         return int(out[0]), int(out[1]), int(out[2])
+
+    TREE_MODES = {0: "hbm-64B", 1: "hbm-32B", 2: "lds-32B", 3: "lds-16B-derived", 4: "lds-16B-derived+hbm-clusters"}
+
+    def trace_config(self) -> dict:
+        """kdpt_trace_config: where the intersect kernel reads the tree, its workgroup, grid and LDS."""
+        m, b, g, l = C.c_int(), C.c_int(), C.c_int(), C.c_longlong()
+        _check(self.lib.kdpt_trace_config(self._ctx, C.byref(m), C.byref(b), C.byref(g), C.byref(l)),
+               "kdpt_trace_config")
+        return {"tree": self.TREE_MODES.get(m.value, str(m.value)), "block": b.value, "grid": g.value,
+                "lds_tree_bytes": l.value}
 
     def trace_grid_share(self) -> float:
         return float(self.stats().intersect_grid_share)

@@ -315,7 +315,7 @@ def test_tuning_knobs_keep_parity(kdpt):
         ref = pt.image().copy()
         with pytest.raises(kdpt.KdptError):
             pt.set_tuning("no_such_knob", 1)
-    for name, val in (("tree_global", 1), ("early_walk", 0), ("early_leaf", 65), ("chunk_width0", 64),
+    for name, val in (("tree_global", 1), ("tree_format", 32), ("tree_format", 16), ("early_walk", 0), ("early_leaf", 65), ("chunk_width0", 64),
                       ("chunk_width1", 8), ("trace_grid_frac", 0.1), ("shade_fused", 0), ("shade_batch", 0),
                       ("gen_geoms", 0)):
         with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
@@ -323,3 +323,32 @@ def test_tuning_knobs_keep_parity(kdpt):
             pt.trace_iterations(1, 8, pipeline=2, batch=4)
             pt.synchronize()
             assert np.array_equal(pt.image().view(np.uint32), ref.view(np.uint32)), name
+
+
+@pytest.mark.parametrize("mesh,level,fmt,want", [("dragon_5", None, 16, "lds-16B-derived"),
+                                                 (None, 6, 0, "lds-16B-derived"),
+                                                 (None, 7, 0, "lds-16B-derived+hbm-clusters")])
+def test_derived_box_tree_in_lds(kdpt, oracle, mesh, level, fmt, want):
+    """The 16-byte NodesDerived records (boxes derived on the walk): the default LDS route for trees whose
+    32-byte copy does not fit (the icosphere's big leaves; its cluster boxes then stay in HBM), and on request
+    (tree_format 16) for the reference's meshes.  Images equal the oracle's and the 32-byte / HBM route's bit
+    for bit."""
+    from kdtreepathtraceroptimization_amd.meshes import attach_icosphere
+    desc = load_fixture_scene("cornell", mesh, res=(64, 48), depth=8)
+    if level is not None:
+        desc = attach_icosphere(desc, level)
+    sd = kdpt.SceneData.from_description(desc)
+    imgs = {}
+    for f in (fmt, 32):
+        with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
+            if f:
+                pt.set_tuning("tree_format", f)
+            cfg = pt.trace_config()
+            if f == fmt:
+                assert cfg["tree"] == want, cfg
+            for it in (1, 2, 3):
+                pt.trace_iteration(it)
+            imgs[f] = pt.image()
+    ref, _ = oracle.OracleScene.from_description(desc).render(1, 3)
+    for f, im in imgs.items():
+        assert np.array_equal(im.view(np.uint32), ref.view(np.uint32)), f
