@@ -929,6 +929,8 @@ struct ShadeArgs {
   const int* ccount;                   // ... per bounce (this iteration's candidate counts)
   // next bounce's intersect-stage first part (prep_ray) for every surviving path, fused here instead of a
   // k_geoms pass: {t_min bits, (geom + 1) | walks << 16} at the path's current slot (k_scatter moves it)
+  int image_zeroed;  // `image` is this iteration's partial image, zeroed by its camera-ray launch: a pixel's
+                     // partialGather then reads +0 (each pixel's path ends once), so its load is skipped
   int prep_on;
   int2* prep;
   int* tile_ccounts;   // [ntiles] walking survivors per tile
@@ -967,7 +969,7 @@ __device__ __attribute__((always_inline)) inline void shade_load(const ShadeArgs
   in.pm = A.paths.pm[i];
   in.hr = A.hits[i];
   in.px_old = make_float3(0.0f, 0.0f, 0.0f);
-  if (COMPACT) {
+  if (COMPACT && !A.image_zeroed) {
     const float* px = A.image + 3 * (size_t)(fbits(in.q1.w) & 0x7fffffff);
     in.px_old = make_float3(px[0], px[1], px[2]);
   }
@@ -1174,7 +1176,9 @@ struct ShadeLDS {
 
 // STAGE: the analytic geoms and the materials copied into LDS (small scenes: their per-lane reads, indexed
 // by hit and by nearest-first order, are then LDS reads instead of L2 round trips)
-template <bool STAGE, int TB>
+// (SYNC false: the caller's next __syncthreads publishes the copy -- k_shade_fused overlaps it with the
+// tile ticket's atomic round trip)
+template <bool STAGE, int TB, bool SYNC = true>
 __device__ __attribute__((always_inline)) inline DevScene stage_scene(const DevScene& S0, ShadeLDS<STAGE, TB>& L) {
   static_assert(sizeof(DevGeom) % 4 == 0 && sizeof(DevMaterial) % 4 == 0, "staged as dwords");
   DevScene S = S0;
@@ -1182,7 +1186,7 @@ __device__ __attribute__((always_inline)) inline DevScene stage_scene(const DevS
     const int gw = S0.num_geoms * (int)(sizeof(DevGeom) / 4), mw = S0.num_materials * (int)(sizeof(DevMaterial) / 4);
     for (int k = threadIdx.x; k < gw; k += TB) L.geoms[k] = reinterpret_cast<const uint32_t*>(S0.geoms)[k];
     for (int k = threadIdx.x; k < mw; k += TB) L.mats[k] = reinterpret_cast<const uint32_t*>(S0.materials)[k];
-    __syncthreads();
+    if (SYNC) __syncthreads();
     S.geoms = reinterpret_cast<const DevGeom*>(L.geoms);
     S.materials = reinterpret_cast<const DevMaterial*>(L.mats);
   }
@@ -1205,7 +1209,7 @@ __device__ __attribute__((always_inline)) inline bool survives(const DevScene& S
 // of an iteration must be started in increasing order (tickets), so every earlier tile is already running.
 template <bool HYBRID, bool STAGE, int TB>
 __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs& A, const FuseArgs& F, const DevScene& S, int tile, int n,
-                                  ShadeLDS<STAGE, TB>& L) {
+                                  ShadeLDS<STAGE, TB>& L, unsigned long long t_wg = 0ull) {
   const int i = tile * TB + threadIdx.x;
   const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
 #ifdef KDPT_SHADE_PROF
@@ -1224,8 +1228,14 @@ __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs
   if (i < n) shade_load<true>(A, S, i, in);
   const bool pred = i < n && survives(S, fbits(in.q2.w), in.hr);
   const unsigned long long ms = __ballot(pred);
+#ifdef KDPT_SHADE_PROF
+  const unsigned long long pa = __builtin_amdgcn_s_memrealtime();
+#endif
   if (lane == 0) L.cnt[0][wid] = (unsigned)__popcll(ms);
   __syncthreads();
+#ifdef KDPT_SHADE_PROF
+  const unsigned long long pb = __builtin_amdgcn_s_memrealtime();
+#endif
   if (wid == 0) {
     unsigned aS = 0;
     for (int w = 0; w < TB / 64; w++) aS += L.cnt[0][w];
@@ -1308,6 +1318,9 @@ __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs
     atomicAdd(&g_shade_prof[2], pt3 - pt2);
     atomicAdd(&g_shade_prof[3], 1ull);
     atomicAdd(&g_shade_prof[4], (unsigned long long)min(TB, n - tile * TB));
+    atomicAdd(&g_shade_prof[5], pt0 - t_wg);  // ticket + staging
+    atomicAdd(&g_shade_prof[6], pa - pt0);    // the path / hit-record loads (thread 0's wave)
+    atomicAdd(&g_shade_prof[7], pb - pa);     // the publication barrier (the tile's slowest wave)
   }
 #endif
 }
@@ -1319,12 +1332,18 @@ __device__ __attribute__((always_inline)) inline void shade_fused_body(const Sha
   // the grid covers every pixel, so past the first bounces most workgroups have no tile: exactly the first
   // ceil(n / SHADE_TB) take tickets (one contended atomic per tile, not per workgroup), the rest leave at once
   if ((int)blockIdx.x * SHADE_TB >= n) return;
+#ifdef KDPT_SHADE_PROF
+  const unsigned long long t_wg = __builtin_amdgcn_s_memrealtime();
+#else
+  const unsigned long long t_wg = 0ull;
+#endif
   __shared__ ShadeLDS<STAGE, SHADE_TB> L;
+  // the ticket's device-scope atomic and the staging copy are in flight together; one barrier for both
   if (threadIdx.x == 0) L.tile = atomicAdd(&F.tickets[A.depth], 1);
+  const DevScene S = stage_scene<STAGE, SHADE_TB, false>(A.S, L);
   __syncthreads();
   const int tile = L.tile;
-  const DevScene S = stage_scene<STAGE, SHADE_TB>(A.S, L);
-  shade_tile<HYBRID, STAGE, SHADE_TB>(A, F, S, tile, n, L);
+  shade_tile<HYBRID, STAGE, SHADE_TB>(A, F, S, tile, n, L, t_wg);
 }
 
 template <bool HYBRID, bool STAGE>
@@ -3245,6 +3264,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       a.paths = c->buf[c->cur];
       a.hits = c->hits;
       a.image = c->image;
+      a.image_zeroed = c->zero_partial ? 1 : 0;
       a.counts = c->counts;
       a.depth = depth;
       a.iter = iters[b];

@@ -1,12 +1,15 @@
 """C5: the ~1M-triangle stress configuration, 1600x1600, depth 16, bounce cap 16.
 
 dragon_8.obj is a missing blob, so the mesh is the synthetic icosphere of meshes.py (level 8:
-1,310,720 triangles, its KD tree has a 29k-triangle leaf, beyond the 32-byte packed node format, so
-the intersect kernel runs on the 64-byte node records from HBM).  Parity: the host KD builder equals
-the reference's own builder (oracle/_ref) on the icosphere written as an OBJ; GPU images equal the
-oracle's bit for bit at sizes the oracle finishes quickly (cap 8 and cap 16); at the full size the
-run is checked through size-independent properties.
+1,310,720 triangles, its KD tree has a 29k-triangle leaf, beyond the 32-byte packed node format; the
+intersect kernel keeps the tree in LDS as 16-byte NodesDerived records and reads the cluster boxes from
+HBM).  Parity: the host KD builder equals the reference's own builder (oracle/_ref) on the icosphere
+written as an OBJ; GPU images equal the oracle's bit for bit at sizes the oracle finishes quickly (cap 8
+and cap 16) and, at the full size, against the oracle's committed render of iteration 1
+(tests/golden/c5_anchor.json, made by tests/golden/make_c5_anchor.py); the full-size run is also checked
+through size-independent properties.
 """
+import json
 import hashlib
 import os
 import tempfile
@@ -76,6 +79,24 @@ def test_icosphere_bit_exact_vs_oracle(kdpt, oracle, level, res, depth, cap, ite
         o = im if o is None else o + im
     assert gs == os_
     assert np.array_equal(g.view(np.uint32), o.view(np.uint32))
+
+
+@pytest.mark.gpu
+def test_c5_full_size_bit_exact_vs_oracle_pin(kdpt):
+    """One full C5 iteration (1600x1600, depth 16, cap 16, 1.31 M triangles) equals the oracle's render
+    committed in c5_anchor.json: sha256 of the float32 image, segments, and the live paths per bounce."""
+    from conftest import TESTS
+    pin = json.load(open(os.path.join(TESTS, "golden", "c5_anchor.json")))
+    desc = load_fixture_scene(pin["scene"], pin["mesh"], res=tuple(pin["res"]), depth=pin["depth"])
+    with kdpt.PathTracer(kdpt.SceneData.from_description(desc), kdpt.default_options(bounce_cap=pin["bounce_cap"]),
+                         device=0) as pt:
+        assert pt.trace_config()["tree"] == "lds-16B-derived+hbm-clusters"
+        pt.trace_iteration(pin["iter"])
+        st = pt.stats()
+        img = pt.image()
+    assert st.segments == pin["segments"]
+    assert [st.seg_per_bounce[d] for d in range(st.bounces)] == pin["seg_per_bounce"]
+    assert hashlib.sha256(np.ascontiguousarray(img, np.float32).tobytes()).hexdigest() == pin["sha256"]
 
 
 @pytest.mark.gpu

@@ -32,7 +32,11 @@ for cfg in sys.argv[1:] or ["8x4", "1x1"]:
     tiles = max(1, out[3])
     print(json.dumps({"cfg": cfg, "iterations": 8 * p * b, "wall_ms": round(wall * 1e3, 2), "tiles": int(out[3]),
                       "paths": int(out[4]),
-                      "us_per_tile": {"shade": round(out[0] / tiles / 100, 2), "lookback": round(out[1] / tiles / 100, 2),
+                      "us_per_tile": {"ticket_stage": round(out[5] / tiles / 100, 2),
+                                      "loads": round(out[6] / tiles / 100, 2),
+                                      "publish_barrier": round(out[7] / tiles / 100, 2),
+                                      "shade_compute": round((out[0] - out[6] - out[7]) / tiles / 100, 2),
+                                      "lookback": round(out[1] / tiles / 100, 2),
                                       "writes": round(out[2] / tiles / 100, 2)},
                       "tile_us_sum_per_iteration": round((out[0] + out[1] + out[2]) / 100 / (8 * p * b), 1)}),
           flush=True)
