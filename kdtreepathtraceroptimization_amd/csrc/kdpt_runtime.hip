@@ -333,10 +333,19 @@ __device__ __attribute__((always_inline)) inline bool prep_ray(const DevScene& S
 // is final here: it is written now, and only the rays that meet the root box are listed (cand, ccount)
 // for the intersect kernel -- whose lanes then all hold rays that actually walk the tree.
 constexpr int GEOM_BLOCK = 1024;  // k_geoms: one candidate-list atomic per 1024 paths
+// k_gen_geoms_b: 256-thread workgroups (one wave per SIMD).  A 1024-thread workgroup needs 4 waves x 88 VGPRs
+// on every SIMD of a CU, which a CU running an intersect workgroup (4 x 96 of 512) never has, so the batch's
+// first launch waited for CUs free of k_trace: 0.93 ms per launch in the pipelined bench against 0.18 ms alone
+// (profiles/r03_ab_log.md); one 88-VGPR wave fits beside the intersect workgroup
+#ifndef KDPT_GEN_BLOCK
+#define KDPT_GEN_BLOCK 256  // tools/build_variant.sh experiments only
+#endif
+constexpr int GEN_BLOCK = KDPT_GEN_BLOCK;
 // One workgroup's part: the analytic geoms + root-box test of its paths (live: the lane holds a path still
 // bouncing), the final hit record of the rays that end there, and the others appended to the candidate list
 // through *ccnt (one atomic per workgroup; a single counter hit once per wave by ~10k waves serialises for
 // ~100 us at 800x800).  Every thread of the workgroup must call it.
+template <int TB = GEOM_BLOCK>
 __device__ __attribute__((always_inline)) inline void geoms_core(const DevScene& S, bool live, int i, f3 o, f3 d,
                                                                  int2* __restrict__ geomhit, int2* __restrict__ hits,
                                                                  int* __restrict__ cand, int* __restrict__ ccnt,
@@ -351,7 +360,7 @@ __device__ __attribute__((always_inline)) inline void geoms_core(const DevScene&
     if (walk) geomhit[i] = make_int2(fbits(t_min), hit);
     else hits[i] = make_int2(hit, -1);  // final: the analytic geoms' hit (code -1: none)
   }
-  __shared__ int s_wcount[GEOM_BLOCK / 64], s_base;
+  __shared__ int s_wcount[TB / 64], s_base;
   const unsigned long long wm = __ballot(walk);
   const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
   if (lane == 0) s_wcount[wv] = __popcll(wm);
@@ -366,7 +375,7 @@ __device__ __attribute__((always_inline)) inline void geoms_core(const DevScene&
   __syncthreads();
   if (threadIdx.x == 0) {
     int tot = 0;
-    for (int w = 0; w < GEOM_BLOCK / 64; w++) {
+    for (int w = 0; w < TB / 64; w++) {
       const int c = s_wcount[w];
       s_wcount[w] = tot;
       tot += c;
@@ -438,7 +447,7 @@ struct GenGeomsBatch {
   GenGeomsIter it[MAXB];
   Counters* count_aabb;
 };
-__global__ __launch_bounds__(GEOM_BLOCK) void k_gen_geoms_b(GenGeomsBatch B) {
+__global__ __launch_bounds__(GEN_BLOCK) void k_gen_geoms_b(GenGeomsBatch B) {
   const GenIter& g = B.g.it[blockIdx.y];
   const GenGeomsIter& q = B.it[blockIdx.y];
   f3 o = mk3(0, 0, 0), d = mk3(0, 0, 1);
@@ -447,7 +456,8 @@ __global__ __launch_bounds__(GEOM_BLOCK) void k_gen_geoms_b(GenGeomsBatch B) {
                                    g.zero_image, o, d);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) *q.ccount0_next = 0;
-  geoms_core(B.S, valid && B.g.traceDepth > 0, i, o, d, q.geomhit, q.hits, q.cand, q.ccount0, B.count_aabb);
+  geoms_core<GEN_BLOCK>(B.S, valid && B.g.traceDepth > 0, i, o, d, q.geomhit, q.hits, q.cand, q.ccount0,
+                        B.count_aabb);
 }
 
 #ifdef KDPT_TAIL_PROF  // tools/build_variant.sh experiments only: intersect workgroup life / tail (ticks)
@@ -3160,7 +3170,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         gg.it[b] = GenGeomsIter{c->cc0_cur, c->ccount0 + (c->gen_parity ^ 1), c->geomhit, c->hits, c->cand};
         c->gen_parity ^= 1;
       }
-      hipLaunchKernelGGL(k_gen_geoms_b, dim3((c0->npix + GEOM_BLOCK - 1) / GEOM_BLOCK, nb), dim3(GEOM_BLOCK), 0, st,
+      hipLaunchKernelGGL(k_gen_geoms_b, dim3((c0->npix + GEN_BLOCK - 1) / GEN_BLOCK, nb), dim3(GEN_BLOCK), 0, st,
                          gg);
     } else {
       hipLaunchKernelGGL(k_gen_rays_b, dim3((c0->npix + 255) / 256, nb), dim3(256), 0, st, gb);
