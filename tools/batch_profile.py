@@ -15,6 +15,9 @@ for cfg in (sys.argv[2] if len(sys.argv) > 2 else "1x1,2x2,1x4").split(","):
     p, b = (int(v) for v in cfg.split("x"))
     pt = PathTracer(sd, default_options(testing_mode=1))
     pt.set_tuning("profile_batches", 2 if os.environ.get("KDPT_PROFILE_STEPS") else 1)
+    for kv in os.environ.get("KDPT_TUNE", "").split(","):  # e.g. KDPT_TUNE=cluster_slab=0
+        if kv:
+            pt.set_tuning(kv.split("=")[0], float(kv.split("=")[1]))
     pt.trace_iterations(1, 4 * p * b, pipeline=p, batch=b)
     pt.synchronize()
     prof = pt.wave_profile()
