@@ -111,12 +111,8 @@ struct DevScene {
   // cluster padded to 64 entries (cluster c = entries [64c, 64c + 64); padding: zeros, index -1)
   const int2* leaf_cl;
   int num_clusters;
-  const float4* cl_lo;  // .w: the slab's low bound (see cl_n)
-  const float4* cl_hi;  // .w: the slab's high bound
-  // unit normal of the cluster's triangles' summed area vectors: every point of its triangles q has
-  // n . (q - c) in [cl_lo.w, cl_hi.w], c = 0.5f * (lo + hi) (bounds rounded outward); n = 0: no slab
-  const float4* cl_n;
-  int cl_slab;  // cull with the slab as well as the box ("cluster_slab" knob; 1 by default)
+  const float4* cl_lo;
+  const float4* cl_hi;
   const int2* cl_info;
   const float4* c_v0;
   const float4* c_e1;
@@ -560,16 +556,13 @@ enum ProfSlot {
 struct ClustersSplit {
   const float4* lo;
   const float4* hi;
-  const float4* n;
   __device__ float4 lo_of(int c) const { return lo[c]; }
   __device__ float4 hi_of(int c) const { return hi[c]; }
-  __device__ float4 n_of(int c) const { return n[c]; }
 };
-struct ClustersInterleaved {  // LDS copy: lo, hi, n per cluster
+struct ClustersInterleaved {
   const float4* p;
-  __device__ float4 lo_of(int c) const { return p[3 * c]; }
-  __device__ float4 hi_of(int c) const { return p[3 * c + 1]; }
-  __device__ float4 n_of(int c) const { return p[3 * c + 2]; }
+  __device__ float4 lo_of(int c) const { return p[2 * c]; }
+  __device__ float4 hi_of(int c) const { return p[2 * c + 1]; }
 };
 
 struct WaveLeafLDS {
@@ -675,31 +668,15 @@ __device__ inline int wave_max_i32(int v) {
 // May the LINE through o (both directions: glm's u/v tests ignore the sign of t) cross the cluster's
 // triangles?  The box is widened by 1e-4 x (distance + size), orders of magnitude above the rounding
 // of the Moller-Trumbore u/v tests, so a culled cluster holds no triangle that would pass them.
-//
-// The slab (when the cluster has one, `slab` wave-uniform): the line's parameter interval through the slab
-// {q : n . (q - c) in [lo.w, hi.w]}, widened by the same margin, must meet its interval through the box.
-// A triangle the line crosses has its crossing point in both (a convex combination of its vertices), so
-// the cull stays conservative; a line parallel to the slab (|n . d| tiny) passes it.  Curved-surface
-// patches are thin along their normal, so a line that only grazes the patch's box is culled.
-__device__ inline bool cluster_may_pass(float4 lo, float4 hi, float4 n, bool slab, f3 o, f3 inv) {
+__device__ inline bool cluster_may_pass(float4 lo, float4 hi, f3 o, f3 inv) {
   const float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
   const float m = 1e-4f * (1.0f + fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) + (hi.x - lo.x) +
                            (hi.y - lo.y) + (hi.z - lo.z));
   const float t1x = (lo.x - m - o.x) * inv.x, t2x = (hi.x + m - o.x) * inv.x;
   const float t1y = (lo.y - m - o.y) * inv.y, t2y = (hi.y + m - o.y) * inv.y;
   const float t1z = (lo.z - m - o.z) * inv.z, t2z = (hi.z + m - o.z) * inv.z;
-  float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
-  float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
-  if (slab) {
-    const float nd = n.x / inv.x + n.y / inv.y + n.z / inv.z;  // n . d (d = 1 / invdir, finite here)
-    const float no = n.x * (o.x - cx) + n.y * (o.y - cy) + n.z * (o.z - cz);
-    if (fabsf(nd) > 1e-12f) {
-      const float rn = 1.0f / nd;
-      const float s1 = (lo.w - m - no) * rn, s2 = (hi.w + m - no) * rn;
-      tmin = fmaxf(tmin, fminf(s1, s2));
-      tmax = fminf(tmax, fmaxf(s1, s2));
-    }
-  }
+  const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
+  const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
   return tmin <= tmax;
 }
 
@@ -990,7 +967,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       if (fastAABB) {
         const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
         const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
-        if (pass) pass = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), clusters.n_of(c), S.cl_slab != 0, oo, ii);
+        if (pass) pass = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
       }
       unsigned long long sm = __ballot(pass);
       int s = -1;

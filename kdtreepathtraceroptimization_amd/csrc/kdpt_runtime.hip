@@ -476,11 +476,7 @@ __device__ unsigned long long g_tail_prof[4];
 #endif
 // (only with the tree in LDS: the 256-thread workgroups of the other modes share CUs anyway, and the C5
 // icosphere, whose tree lives in HBM, lost 3.5 % to the cap)
-#ifndef KDPT_TRACE_WAVES16
-#define KDPT_TRACE_WAVES16 5  // the NodesDerived modes (tools/build_variant.sh experiments)
-#endif
-#define KDPT_TRACE_ATTR \
-  __attribute__((amdgpu_waves_per_eu(MODE >= 3 ? KDPT_TRACE_WAVES16 : (tree_in_lds(MODE) ? KDPT_TRACE_WAVES : 1))))
+#define KDPT_TRACE_ATTR __attribute__((amdgpu_waves_per_eu(tree_in_lds(MODE) ? KDPT_TRACE_WAVES : 1)))
 template <bool HYBRID, bool COUNT, int MODE>
 __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(TraceArgs A) {
   constexpr int TB = trace_block<MODE>();
@@ -503,9 +499,8 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
     if (MODE != TREE_LDS16G) {
       float4* s_cl = reinterpret_cast<float4*>(s_tree + words);
       for (int k = threadIdx.x; k < S.num_clusters; k += TB) {
-        s_cl[3 * k] = S.cl_lo[k];
-        s_cl[3 * k + 1] = S.cl_hi[k];
-        s_cl[3 * k + 2] = S.cl_n[k];
+        s_cl[2 * k] = S.cl_lo[k];
+        s_cl[2 * k + 1] = S.cl_hi[k];
       }
     }
     __syncthreads();
@@ -618,13 +613,13 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
                                    ClustersInterleaved{reinterpret_cast<const float4*>(s_tree + S.num_nodes)}, R,
                                    fastAABB, S.num_materials, cnt, W, P);
       else if (MODE == TREE_LDS16G)
-        trace_phase<HYBRID, COUNT>(S, NodesDerived{s_tree}, ClustersSplit{S.cl_lo, S.cl_hi, S.cl_n}, R, fastAABB,
+        trace_phase<HYBRID, COUNT>(S, NodesDerived{s_tree}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
                                    S.num_materials, cnt, W, P);
       else if (MODE == TREE_PACKED)
-        trace_phase<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ClustersSplit{S.cl_lo, S.cl_hi, S.cl_n}, R, fastAABB,
+        trace_phase<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
                                    S.num_materials, cnt, W, P);
       else
-        trace_phase<HYBRID, COUNT>(S, NodesWide{S.nodes}, ClustersSplit{S.cl_lo, S.cl_hi, S.cl_n}, R, fastAABB,
+        trace_phase<HYBRID, COUNT>(S, NodesWide{S.nodes}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
                                    S.num_materials, cnt, W, P);
     }
     // ---- finished rays: their hit record (what ShadeableIntersection would carry) ----
@@ -832,8 +827,7 @@ __global__ __launch_bounds__(TILE) void k_brute(BruteArgs A) {
           // can hit; the others test its triangles in file order as before
           for (int k = k0; k < k0 + nt;) {
             const int j = k >> 6, kend = min(k0 + nt, (j + 1) << 6);
-            const bool may = take && (!cull || cluster_may_pass(A.chunk_lo[j], A.chunk_hi[j], make_float4(0.0f, 0.0f, 0.0f, 0.0f),
-                                                                      false, o, inv));
+            const bool may = take && (!cull || cluster_may_pass(A.chunk_lo[j], A.chunk_hi[j], o, inv));
             if (__any(may)) {
               for (; k < kend; k++) {
                 const TriData T = tri_load(S, k);
@@ -1912,7 +1906,7 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
                    const std::vector<float4>& e2, std::vector<int2>& leaf_cl) {
   const int nn = sc->num_nodes;
   leaf_cl.assign(nn, make_int2(0, 0));
-  std::vector<float4> lo, hi, nrm, cv0, ce1, ce2;
+  std::vector<float4> lo, hi, cv0, ce1, ce2;
   std::vector<int2> info;
   auto spread = [](uint32_t v) {
     uint32_t r = 0;
@@ -1962,48 +1956,15 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
         ce1.push_back(make_float4(0.0f, 0.0f, 0.0f, ibits(-1)));
         ce2.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
       }
-      // the slab: n = the normalised sum of the triangles' (v1 - v0) x (v2 - v0), c as the kernel forms it,
-      // [min, max] of n . (v - c) over the vertices in double, rounded outward to float
-      const float cc[3] = {0.5f * (l[0] + h[0]), 0.5f * (l[1] + h[1]), 0.5f * (l[2] + h[2])};
-      double ns[3] = {0, 0, 0};
-      for (int k = b; k < b + cnt; k++) {
-        const kdpt_tri_bare& T = sc->tris[start + key[k].second];
-        const double ax = (double)T.x2 - T.x1, ay = (double)T.y2 - T.y1, az = (double)T.z2 - T.z1;
-        const double bx = (double)T.x3 - T.x1, by = (double)T.y3 - T.y1, bz = (double)T.z3 - T.z1;
-        ns[0] += ay * bz - az * by;
-        ns[1] += az * bx - ax * bz;
-        ns[2] += ax * by - ay * bx;
-      }
-      const double nl = std::sqrt(ns[0] * ns[0] + ns[1] * ns[1] + ns[2] * ns[2]);
-      float nf[3] = {0.0f, 0.0f, 0.0f};
-      float dlo = -FLT_MAXV, dhi = FLT_MAXV;
-      if (nl > 0 && std::isfinite(nl)) {
-        for (int a = 0; a < 3; a++) nf[a] = (float)(ns[a] / nl);
-        double mn = 1e300, mx = -1e300;
-        for (int k = b; k < b + cnt; k++) {
-          const kdpt_tri_bare& T = sc->tris[start + key[k].second];
-          const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
-          for (int v = 0; v < 3; v++) {
-            const double d = (double)nf[0] * ((double)vx[v] - cc[0]) + (double)nf[1] * ((double)vy[v] - cc[1]) +
-                             (double)nf[2] * ((double)vz[v] - cc[2]);
-            mn = std::min(mn, d);
-            mx = std::max(mx, d);
-          }
-        }
-        dlo = std::nextafter((float)mn, -FLT_MAXV);
-        dhi = std::nextafter((float)mx, FLT_MAXV);
-      }
-      lo.push_back(make_float4(l[0], l[1], l[2], dlo));
-      hi.push_back(make_float4(h[0], h[1], h[2], dhi));
-      nrm.push_back(make_float4(nf[0], nf[1], nf[2], 0.0f));
+      lo.push_back(make_float4(l[0], l[1], l[2], 0.0f));
+      hi.push_back(make_float4(h[0], h[1], h[2], 0.0f));
     }
   }
   int2 *dl, *di;
-  float4 *dlo, *dhi, *dn, *dv0, *de1, *de2;
+  float4 *dlo, *dhi, *dv0, *de1, *de2;
   int rc;
   if ((rc = dupload(c, &dl, leaf_cl.data(), leaf_cl.size())) || (rc = dupload(c, &di, info.data(), info.size())) ||
       (rc = dupload(c, &dlo, lo.data(), lo.size())) || (rc = dupload(c, &dhi, hi.data(), hi.size())) ||
-      (rc = dupload(c, &dn, nrm.data(), nrm.size())) ||
       (rc = dupload(c, &dv0, cv0.data(), cv0.size())) || (rc = dupload(c, &de1, ce1.data(), ce1.size())) ||
       (rc = dupload(c, &de2, ce2.data(), ce2.size())))
     return rc;
@@ -2012,8 +1973,6 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
   c->S.cl_info = di;
   c->S.cl_lo = dlo;
   c->S.cl_hi = dhi;
-  c->S.cl_n = dn;
-  c->S.cl_slab = 1;
   c->S.c_v0 = dv0;
   c->S.c_e1 = de1;
   c->S.c_e2 = de2;
@@ -2122,7 +2081,7 @@ int setup_trace(kdpt_ctx* c) {
   const size_t lds_max = prop.sharedMemPerBlock > 0 ? prop.sharedMemPerBlock : 65536;
   // (the counting kernel's per-wave WaveProf too: the tree must fit next to either kernel's static part)
   const size_t per_wave = sizeof(WaveLeafLDS) + sizeof(WaveProf);
-  const size_t cl_bytes = 48 * (size_t)c->S.num_clusters;  // lo, hi, n
+  const size_t cl_bytes = 32 * (size_t)c->S.num_clusters;
   struct Cand { int mode; size_t lds; };
   std::vector<Cand> cands;
   // (in order of preference at equal occupancy: the 32-byte records need no box bookkeeping on the walk, which
@@ -2628,8 +2587,6 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     int rc = setup_trace(c);
     if (rc) return rc;
     if (c->grid_env) c->trace_grid = std::max(1, (int)(c->full_trace_grid * frac));
-  } else if (k == "cluster_slab") {
-    c->S.cl_slab = v != 0;
   } else if (k == "profile_batches") {
     c->profile_batches = v != 0;
     c->profile_steps = v >= 2;

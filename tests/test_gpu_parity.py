@@ -315,7 +315,7 @@ def test_tuning_knobs_keep_parity(kdpt):
         ref = pt.image().copy()
         with pytest.raises(kdpt.KdptError):
             pt.set_tuning("no_such_knob", 1)
-    for name, val in (("tree_global", 1), ("tree_format", 32), ("tree_format", 16), ("cluster_slab", 0), ("early_walk", 0), ("early_leaf", 65), ("chunk_width0", 64),
+    for name, val in (("tree_global", 1), ("tree_format", 32), ("tree_format", 16), ("early_walk", 0), ("early_leaf", 65), ("chunk_width0", 64),
                       ("chunk_width1", 8), ("trace_grid_frac", 0.1), ("shade_fused", 0), ("shade_batch", 0),
                       ("gen_geoms", 0)):
         with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
@@ -326,7 +326,7 @@ def test_tuning_knobs_keep_parity(kdpt):
 
 
 @pytest.mark.parametrize("mesh,level,fmt,want", [("dragon_5", None, 16, "lds-16B-derived"),
-                                                 (None, 6, 0, "lds-16B-derived+hbm-clusters"),
+                                                 (None, 6, 0, "lds-16B-derived"),
                                                  (None, 7, 0, "lds-16B-derived+hbm-clusters")])
 def test_derived_box_tree_in_lds(kdpt, oracle, mesh, level, fmt, want):
     """The 16-byte NodesDerived records (boxes derived on the walk): the default LDS route for trees whose
