@@ -332,11 +332,11 @@ __device__ __attribute__((always_inline)) inline bool prep_ray(const DevScene& S
 // effect (traverseKDbareShortHybrid: `!hitGeom && parentID == -1` -> break), so such a ray's hit record
 // is final here: it is written now, and only the rays that meet the root box are listed (cand, ccount)
 // for the intersect kernel -- whose lanes then all hold rays that actually walk the tree.
-constexpr int GEOM_BLOCK = 1024;  // k_geoms: one candidate-list atomic per 1024 paths
-// k_gen_geoms_b: 256-thread workgroups (one wave per SIMD).  A 1024-thread workgroup needs 4 waves x 88 VGPRs
-// on every SIMD of a CU, which a CU running an intersect workgroup (4 x 96 of 512) never has, so the batch's
-// first launch waited for CUs free of k_trace: 0.93 ms per launch in the pipelined bench against 0.18 ms alone
-// (profiles/r03_ab_log.md); one 88-VGPR wave fits beside the intersect workgroup
+// k_gen_geoms_b / k_geoms_b: 256-thread workgroups (one wave per SIMD), one candidate-list atomic per
+// workgroup.  A 1024-thread workgroup needs 4 waves x 88 VGPRs on every SIMD of a CU, which a CU running an
+// intersect workgroup (4 x 96 of 512) never has, so the batch's first launch waited for CUs free of k_trace:
+// 0.93 ms per launch in the pipelined bench against 0.18 ms alone (profiles/r03_ab_log.md); one 88-VGPR
+// wave fits beside the intersect workgroup
 #ifndef KDPT_GEN_BLOCK
 #define KDPT_GEN_BLOCK 256  // tools/build_variant.sh experiments only
 #endif
@@ -345,7 +345,7 @@ constexpr int GEN_BLOCK = KDPT_GEN_BLOCK;
 // bouncing), the final hit record of the rays that end there, and the others appended to the candidate list
 // through *ccnt (one atomic per workgroup; a single counter hit once per wave by ~10k waves serialises for
 // ~100 us at 800x800).  Every thread of the workgroup must call it.
-template <int TB = GEOM_BLOCK>
+template <int TB = GEN_BLOCK>
 __device__ __attribute__((always_inline)) inline void geoms_core(const DevScene& S, bool live, int i, f3 o, f3 d,
                                                                  int2* __restrict__ geomhit, int2* __restrict__ hits,
                                                                  int* __restrict__ cand, int* __restrict__ ccnt,
@@ -403,7 +403,7 @@ __device__ __attribute__((always_inline)) inline void geoms_body(const DevScene&
     o = mk3(q0.x, q0.y, q0.z);
     d = mk3(q1.x, q1.y, q1.z);
   }
-  geoms_core(S, live, i, o, d, geomhit, hits, cand, ccount + depth, count_aabb);
+  geoms_core<GEN_BLOCK>(S, live, i, o, d, geomhit, hits, cand, ccount + depth, count_aabb);
   if (threadIdx.x == 0) atomicMax(&gspan[2 * depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
@@ -423,7 +423,7 @@ struct GeomsBatch {
   Counters* count_aabb;
   unsigned long long* gspan;
 };
-__global__ __launch_bounds__(GEOM_BLOCK) void k_geoms_b(GeomsBatch B) {
+__global__ __launch_bounds__(GEN_BLOCK) void k_geoms_b(GeomsBatch B) {
   const GeomsIter& g = B.it[blockIdx.y];
   geoms_body(B.S, g.paths, g.counts, B.depth, g.geomhit, g.hits, g.cand, g.ccount, B.count_aabb, B.gspan);
 }
@@ -1381,8 +1381,11 @@ struct ScanJob {
   int nkeys;
   int* total_out;
 };
-__global__ __launch_bounds__(1024) void k_scan(ScanJob j0, ScanJob j1, const int* counts, int depth,
-                                               int ntiles_alloc) {
+// 256 threads: every kernel a batch launches fits beside a resident intersect workgroup (4 waves x 96 VGPRs per
+// SIMD, 150 KB of LDS per CU), which a 1024-thread workgroup never does
+constexpr int SCAN_TB = 256;
+__global__ __launch_bounds__(SCAN_TB) void k_scan(ScanJob j0, ScanJob j1, const int* counts, int depth,
+                                                  int ntiles_alloc) {
   const ScanJob& J = blockIdx.x == 0 ? j0 : j1;
   const int* __restrict__ tile_counts = J.tile_counts;
   int* __restrict__ tile_off = J.tile_off;
@@ -1391,11 +1394,11 @@ __global__ __launch_bounds__(1024) void k_scan(ScanJob j0, ScanJob j1, const int
   const int n = counts[depth];
   const int ntiles = (n + TILE - 1) / TILE;
   const int total_entries = nkeys * ntiles;
-  __shared__ int s_wave[16];
+  __shared__ int s_wave[SCAN_TB / 64];
   __shared__ int s_carry;
   if (threadIdx.x == 0) s_carry = 0;
   __syncthreads();
-  for (int base = 0; base < total_entries; base += 1024) {
+  for (int base = 0; base < total_entries; base += SCAN_TB) {
     const int e = base + threadIdx.x;
     int v = 0;
     int k = 0, t = 0;
@@ -1414,19 +1417,19 @@ __global__ __launch_bounds__(1024) void k_scan(ScanJob j0, ScanJob j1, const int
     if (lane == 63) s_wave[wid] = x;
     __syncthreads();
     if (wid == 0) {
-      int w = lane < 16 ? s_wave[lane] : 0;
-      for (int off = 1; off < 16; off <<= 1) {
+      int w = lane < SCAN_TB / 64 ? s_wave[lane] : 0;
+      for (int off = 1; off < SCAN_TB / 64; off <<= 1) {
         int y = __shfl_up(w, off);
         if (lane >= off) w += y;
       }
-      if (lane < 16) s_wave[lane] = w;
+      if (lane < SCAN_TB / 64) s_wave[lane] = w;
     }
     __syncthreads();
     const int carry = s_carry;
     const int excl = carry + (wid > 0 ? s_wave[wid - 1] : 0) + x - v;
     if (e < total_entries) tile_off[k * ntiles_alloc + t] = excl;
     __syncthreads();
-    if (threadIdx.x == 1023) s_carry = excl + v;
+    if (threadIdx.x == SCAN_TB - 1) s_carry = excl + v;
     __syncthreads();
   }
   if (threadIdx.x == 0 && total_out) *total_out = s_carry;
@@ -3250,7 +3253,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
           kdpt_ctx* c = cs[b];
           gb.it[b] = GeomsIter{c->buf[c->cur], c->counts, c->geomhit, c->hits, c->cand, c->ccount};
         }
-        hipLaunchKernelGGL(k_geoms_b, dim3((c0->npix + GEOM_BLOCK - 1) / GEOM_BLOCK, nb), dim3(GEOM_BLOCK), 0, st, gb);
+        hipLaunchKernelGGL(k_geoms_b, dim3((c0->npix + GEN_BLOCK - 1) / GEN_BLOCK, nb), dim3(GEN_BLOCK), 0, st, gb);
         HIP_TRY(hipGetLastError());
       }
       launch_trace(c0, t, count, st);
@@ -3328,7 +3331,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         // offsets per tile + the next bounce's candidate count (a second workgroup)
         const ScanJob j0{c->tile_counts, c->tile_off, sort ? c->nkeys : 1, c->counts + depth + 1};
         const ScanJob j1{c->tile_ccounts, c->tile_coff, 1, c->ccount + depth + 1};
-        hipLaunchKernelGGL(k_scan, dim3(prep_next ? 2 : 1), dim3(1024), 0, st, j0, j1, c->counts, depth, c->ntiles);
+        hipLaunchKernelGGL(k_scan, dim3(prep_next ? 2 : 1), dim3(SCAN_TB), 0, st, j0, j1, c->counts, depth, c->ntiles);
         HIP_TRY(hipGetLastError());
         const int nxt = c->cur ^ 1;
         ScatterPrep sp{prep_next ? 1 : 0, c->prep, c->geomhit, c->hits, c->cand, c->tile_coff};
