@@ -16,7 +16,8 @@ if [ -n "$KDPT_REV" ]; then
   SRC="$SRC/kdtreepathtraceroptimization_amd/csrc"
 fi
 # the product's device code-generation flags (scheduler), so a variant differs from libkdpt.so only by "$@"
-DEVICE_FLAGS=$(cd "$ROOT" && python3 -m kdtreepathtraceroptimization_amd._build --device-flags)
+# (KDPT_DEVICE_FLAGS overrides them, e.g. KDPT_DEVICE_FLAGS=" " for the default machine scheduler)
+DEVICE_FLAGS=${KDPT_DEVICE_FLAGS:-$(cd "$ROOT" && python3 -m kdtreepathtraceroptimization_amd._build --device-flags)}
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -ffp-contract=off -fno-fast-math -I "$ROOT/include" $DEVICE_FLAGS "$@" \
   -c "$SRC/kdpt_runtime.hip" -o "$ROOT/build/ab/$NAME.o"
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$ROOT/ab/$NAME.so" "$ROOT/build/ab/$NAME.o" \
