@@ -114,6 +114,18 @@ struct DevScene {
   const float4* cl_lo;
   const float4* cl_hi;
   const int2* cl_info;
+  // super-clusters: a big leaf's clusters in runs of SUPER (consecutive in Morton order), as 16-byte records:
+  // the box in half precision rounded outward (lo.x | lo.y << 16, lo.z | hi.x << 16, hi.y | hi.z << 16) and
+  // first cluster << 5 | (count - 1); snodes = the NodesDerived records with a big leaf's first super instead
+  // of its first cluster (TREE_LDS16S: records and supers in LDS, the two-level cull), or null
+  const int4* sup;
+  int num_supers;
+  // per cluster: the unit normal of its triangles' summed area vectors (xyz); every point q of its triangles
+  // has n . (q - c) in [cl_lo.w, cl_hi.w], c = 0.5f * (lo + hi) (bounds rounded outward); n = 0: no slab.
+  // The two-level cull tests the line against this slab as well as the box (knob "cluster_slab")
+  const float4* cl_n;
+  int cl_slab;
+  const int4* snodes;
   const float4* c_v0;
   const float4* c_e1;
   const float4* c_e2;
@@ -549,21 +561,50 @@ enum ProfSlot {
   PROF_NODE_TRIPS, PROF_NODE_CYC, PROF_BIG_SWEEPS, PROF_BIG_CYC, PROF_SMALL_PHASES, PROF_SMALL_ROUNDS,
   PROF_SMALL_CYC, PROF_FINAL_CYC, PROF_SETUP_CYC, PROF_GEOM_CYC, PROF_POST_CYC, PROF_SPARE,
   PROF_BIG_LEAVES, PROF_BIG_CLUSTERS, PROF_BIG_PASS, PROF_BIG_MULTI, PROF_SMALL_PAIRS, PROF_NODE_LEAFWAIT,
-  PROF_NODE_DONE, PROF_TAIL_CYC, PROF_TAIL_NODE_DONE, PROF_SLOTS
+  PROF_NODE_DONE, PROF_TAIL_CYC, PROF_TAIL_NODE_DONE, PROF_BIG_SUPERS, PROF_BIG_CULL_CYC, PROF_SLOTS
 };
 
 // Cluster boxes of the big leaves: separate lo/hi arrays (HBM) or interleaved lo, hi (LDS copy).
 struct ClustersSplit {
+  static constexpr bool kSuper = false;
   const float4* lo;
   const float4* hi;
   __device__ float4 lo_of(int c) const { return lo[c]; }
   __device__ float4 hi_of(int c) const { return hi[c]; }
 };
 struct ClustersInterleaved {
+  static constexpr bool kSuper = false;
   const float4* p;
   __device__ float4 lo_of(int c) const { return p[2 * c]; }
   __device__ float4 hi_of(int c) const { return p[2 * c + 1]; }
 };
+// Two-level: the super-cluster records in LDS (16 bytes: half-precision box rounded outward, first cluster
+// and count), the cluster boxes in HBM/L2.
+__device__ inline float half_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu)); }
+__device__ inline float half_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
+struct ClustersSuper {
+  static constexpr bool kSuper = true;
+  const int4* sp;
+  const float4* lo;
+  const float4* hi;
+  const float4* n;  // slab normals (DevScene::cl_n)
+  __device__ float4 n_of(int c) const { return n[c]; }
+  // box of super k, and its first cluster << 5 | count - 1
+  __device__ uint32_t sup(int k, float4& l, float4& h) const {
+    typedef int v4i __attribute__((ext_vector_type(4)));
+    const v4i q = reinterpret_cast<const v4i*>(sp)[k];  // one 16-byte LDS load
+    const uint32_t w0 = (uint32_t)q.x, w1 = (uint32_t)q.y, w2 = (uint32_t)q.z;
+    l = make_float4(half_lo(w0), half_hi(w0), half_lo(w1), 0.0f);
+    h = make_float4(half_hi(w1), half_lo(w2), half_hi(w2), 0.0f);
+    return (uint32_t)q.w;
+  }
+  __device__ float4 lo_of(int c) const { return lo[c]; }
+  __device__ float4 hi_of(int c) const { return hi[c]; }
+};
+#ifndef KDPT_SUPER
+#define KDPT_SUPER 16  // tools/build_variant.sh experiments only (a power of two <= 64)
+#endif
+constexpr int SUPER = KDPT_SUPER;  // clusters per super-cluster
 
 struct WaveLeafLDS {
   int slot[64];    // pair_owner's scatter slots (all zero between calls)
@@ -600,6 +641,11 @@ __device__ inline void prof_lap(WaveProf* P, int k) {  // cycles since the last 
 #define KDPT_BIG_LEAF 64  // tools/build_variant.sh experiments only
 #endif
 constexpr int BIG_LEAF = KDPT_BIG_LEAF;  // leaves this size or larger are tested cluster by cluster
+
+// number of set bits of mask below this lane
+__device__ inline unsigned int lane_prefix(unsigned long long mask) {
+  return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
+}
 
 __device__ inline float readlane_f(float v, int lane) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
@@ -677,6 +723,31 @@ __device__ inline bool cluster_may_pass(float4 lo, float4 hi, f3 o, f3 inv) {
   const float t1z = (lo.z - m - o.z) * inv.z, t2z = (hi.z + m - o.z) * inv.z;
   const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
   const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+  return tmin <= tmax;
+}
+
+// cluster_may_pass and the cluster's slab {q : n . (q - c) in [lo.w, hi.w]}: the line's parameter interval
+// through the slab, widened by the same margin, must meet its interval through the box.  A triangle the line
+// crosses has its crossing point in both (a convex combination of its vertices), so the cull stays
+// conservative; a line (nearly) parallel to the slab passes it.  A curved-surface patch is thin along its
+// normal, so a line that only grazes the patch's box is culled.
+__device__ inline bool cluster_may_pass_slab(float4 lo, float4 hi, float4 n, f3 o, f3 inv, f3 d) {
+  const float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
+  const float m = 1e-4f * (1.0f + fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) + (hi.x - lo.x) +
+                           (hi.y - lo.y) + (hi.z - lo.z));
+  const float t1x = (lo.x - m - o.x) * inv.x, t2x = (hi.x + m - o.x) * inv.x;
+  const float t1y = (lo.y - m - o.y) * inv.y, t2y = (hi.y + m - o.y) * inv.y;
+  const float t1z = (lo.z - m - o.z) * inv.z, t2z = (hi.z + m - o.z) * inv.z;
+  float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
+  float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+  const float nd = n.x * d.x + n.y * d.y + n.z * d.z;
+  const float no = n.x * (o.x - cx) + n.y * (o.y - cy) + n.z * (o.z - cz);
+  if (fabsf(nd) > 1e-12f) {
+    const float rn = 1.0f / nd;
+    const float s1 = (lo.w - m - no) * rn, s2 = (hi.w + m - no) * rn;
+    tmin = fmaxf(tmin, fminf(s1, s2));
+    tmax = fminf(tmax, fmaxf(s1, s2));
+  }
   return tmin <= tmax;
 }
 
@@ -946,29 +1017,12 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   // index, last hit = max, best = min (t, index).
   const bool big = leaf && lsize >= BIG_LEAF;
   if (__any(big)) {
-    const int ncl = big ? (lsize + 63) >> 6 : 0;
-    const int cfirst = big ? (NodeSrc::kLeafHoldsCluster ? lstart : S.leaf_cl[lnode].x) : 0;
-    const int incl = wave_incl_scan<false>(ncl);
-    const int P = __builtin_amdgcn_readlane(incl, 63);
-    const int excl = incl - ncl;
-    W->tbase[lane] = cfirst - excl;  // cluster of pair q = tbase[owner] + q
-    wave_lds_sync();
-    if (COUNT) {
-      prof_add(WP, PROF_BIG_LEAVES, (unsigned long long)__popcll(__ballot(big)));
-      prof_add(WP, PROF_BIG_CLUSTERS, (unsigned long long)P);
-    }
     unsigned long long k_pass = 0ull, k_best = ~0ull;
     int k_lasthit = -1, k_nhit = 0;
-    int carry = 0;
-    for (int B = 0; B < P; B += 64) {
-      const int own = pair_owner(W->slot, excl, ncl, B, carry);
-      const int c = W->tbase[own] + B + lane;
-      bool pass = B + lane < P;
-      if (fastAABB) {
-        const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
-        const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
-        if (pass) pass = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
-      }
+    // Sweeps of the (ray, cluster) pairs `pass` marks: cluster c with the ray of lane own, each surviving
+    // cluster by the whole wave, the next survivor's triangles fetched while this one is tested; the results
+    // are folded into the owner lane's k_* (order-free).  Wave-uniform call.
+    auto sweep = [&](bool pass, int c, int own) {
       unsigned long long sm = __ballot(pass);
       int s = -1;
       TriData T{};
@@ -1027,6 +1081,101 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         }
         s = sn;
         T = Tn;
+      }
+    };
+    const int ncl = big ? (lsize + 63) >> 6 : 0;
+    if constexpr (ClusterSrc::kSuper) {
+      // Two levels (leaves of thousands of triangles, e.g. the C5 icosphere's): the (ray, super-cluster) pairs
+      // are culled first, 64 per pass, against the supers' boxes (LDS); each surviving super's SUPER clusters
+      // are then culled against their own boxes, 64 / SUPER supers per round, and the survivors swept.  A
+      // super's box holds its clusters' boxes, so the second level sees every cluster the one-level cull
+      // would pass.
+      const int nsp = (ncl + SUPER - 1) / SUPER;
+      const int incl = wave_incl_scan<false>(nsp);
+      const int P = __builtin_amdgcn_readlane(incl, 63);
+      const int excl = incl - nsp;
+      W->tbase[lane] = lstart - excl;  // super of pair q = tbase[owner] + q (lstart: the leaf's first super)
+      wave_lds_sync();
+      if (COUNT) {
+        prof_add(WP, PROF_BIG_LEAVES, (unsigned long long)__popcll(__ballot(big)));
+        prof_add(WP, PROF_BIG_SUPERS, (unsigned long long)P);
+      }
+      // one pass's surviving supers, {owner << 32 | first cluster << 5 | count - 1}, in W->best (the
+      // small-leaf phase below initialises it afresh)
+      static_assert(SUPER <= 32 && 64 % SUPER == 0, "super-cluster size");
+      unsigned long long* slist = W->best;
+      int carry = 0;
+      for (int B = 0; B < P; B += 64) {
+        const int own = pair_owner(W->slot, excl, nsp, B, carry);
+        const int sp = W->tbase[own] + B + lane;
+        bool pass = B + lane < P;
+        float4 slo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), shi = slo;
+        uint32_t sinfo = 0u;
+        if (pass) sinfo = clusters.sup(sp, slo, shi);
+        if (fastAABB) {
+          const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
+          const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
+          if (pass) pass = cluster_may_pass(slo, shi, oo, ii);
+        }
+        const unsigned long long sm = __ballot(pass);
+        const int nsv = __popcll(sm);
+        if (pass)
+          slist[lane_prefix(sm)] = ((unsigned long long)(uint32_t)own << 32) | sinfo;
+        wave_lds_sync();
+        for (int q = 0; q < nsv; q += 64 / SUPER) {
+          const int e = q + lane / SUPER, k = lane % SUPER;
+          bool cp = e < nsv;
+          int cown = 0, c = 0;
+          if (cp) {
+            const unsigned long long ent = slist[e];
+            cown = (int)(ent >> 32);
+            c = (int)((uint32_t)ent >> 5) + k;
+            cp = k <= (int)((uint32_t)ent & 31u);
+          }
+          if (COUNT) prof_add(WP, PROF_BIG_CLUSTERS, (unsigned long long)__popcll(__ballot(cp)));
+          if (fastAABB) {
+            const f3 oo = mk3(bpermute_f(o.x, cown), bpermute_f(o.y, cown), bpermute_f(o.z, cown));
+            const f3 ii =
+                mk3(bpermute_f(invdir.x, cown), bpermute_f(invdir.y, cown), bpermute_f(invdir.z, cown));
+            if (S.cl_slab) {
+              const f3 dd = mk3(bpermute_f(d.x, cown), bpermute_f(d.y, cown), bpermute_f(d.z, cown));
+              if (cp) cp = cluster_may_pass_slab(clusters.lo_of(c), clusters.hi_of(c), clusters.n_of(c), oo, ii, dd);
+            } else {
+              if (cp) cp = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
+            }
+          }
+          if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
+          sweep(cp, c, cown);
+          if (COUNT) prof_lap(WP, PROF_BIG_CYC);
+        }
+        wave_lds_sync();  // slist is rewritten by the next pass
+      }
+    } else {
+      // One level: lane L owns the (ray, cluster) pairs [excl_L, excl_L + ncl_L); one pass culls 64 of them
+      // against the cluster boxes (the line misses the box: no triangle of it passes the u/v tests).
+      const int cfirst = big ? (NodeSrc::kLeafHoldsCluster ? lstart : S.leaf_cl[lnode].x) : 0;
+      const int incl = wave_incl_scan<false>(ncl);
+      const int P = __builtin_amdgcn_readlane(incl, 63);
+      const int excl = incl - ncl;
+      W->tbase[lane] = cfirst - excl;  // cluster of pair q = tbase[owner] + q
+      wave_lds_sync();
+      if (COUNT) {
+        prof_add(WP, PROF_BIG_LEAVES, (unsigned long long)__popcll(__ballot(big)));
+        prof_add(WP, PROF_BIG_CLUSTERS, (unsigned long long)P);
+      }
+      int carry = 0;
+      for (int B = 0; B < P; B += 64) {
+        const int own = pair_owner(W->slot, excl, ncl, B, carry);
+        const int c = W->tbase[own] + B + lane;
+        bool pass = B + lane < P;
+        if (fastAABB) {
+          const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
+          const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
+          if (pass) pass = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
+        }
+        if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
+        sweep(pass, c, own);
+        if (COUNT) prof_lap(WP, PROF_BIG_CYC);
       }
     }
     if (big) {

@@ -75,10 +75,6 @@ struct Counters {
                                                   // the box diagonal): does the chord predict a ray's cost?
 };
 
-__device__ inline unsigned int lane_prefix(unsigned long long mask) {
-  return __builtin_amdgcn_mbcnt_hi((unsigned)(mask >> 32), __builtin_amdgcn_mbcnt_lo((unsigned)mask, 0u));
-}
-
 // ---------------------------------------------------------------------------
 // generateRayFromCamera (src/pathtrace.cu:315-397)
 // ---------------------------------------------------------------------------
@@ -173,8 +169,10 @@ struct GenIter {
 // ---------------------------------------------------------------------------
 // TREE_LDS: 32-byte NodesPacked records in LDS (+ the cluster boxes); TREE_LDS16: 16-byte NodesDerived
 // records + cluster boxes in LDS; TREE_LDS16G: NodesDerived in LDS, cluster boxes in HBM/L2 (trees whose
-// clusters do not fit, e.g. the C5 icosphere: 2 655 nodes = 41 KB, 22 848 clusters = 714 KB)
-enum TreeMode { TREE_WIDE = 0, TREE_PACKED = 1, TREE_LDS = 2, TREE_LDS16 = 3, TREE_LDS16G = 4 };
+// clusters do not fit, e.g. the C5 icosphere: 2 655 nodes = 41 KB, 22 848 clusters = 714 KB); TREE_LDS16S:
+// NodesDerived + the super-cluster boxes in LDS, cluster boxes in HBM/L2, two-level cull (the C5 icosphere:
+// 1 430 supers of 16 clusters = 45 KB)
+enum TreeMode { TREE_WIDE = 0, TREE_PACKED = 1, TREE_LDS = 2, TREE_LDS16 = 3, TREE_LDS16G = 4, TREE_LDS16S = 5 };
 #ifndef KDPT_TRACE_BLOCK
 #define KDPT_TRACE_BLOCK 1024  // tools/build_variant.sh experiments only
 #endif
@@ -494,9 +492,11 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
   if (tree_in_lds(MODE)) {
     if (n == 0) return;  // uniform: nothing to trace
     const int words = NODE_WORDS * S.num_nodes;
-    const int4* src = MODE == TREE_LDS ? S.pnodes : S.dnodes;
+    const int4* src = MODE == TREE_LDS ? S.pnodes : (MODE == TREE_LDS16S ? S.snodes : S.dnodes);
     for (int k = threadIdx.x; k < words; k += TB) s_tree[k] = src[k];
-    if (MODE != TREE_LDS16G) {
+    if (MODE == TREE_LDS16S) {
+      for (int k = threadIdx.x; k < S.num_supers; k += TB) s_tree[words + k] = S.sup[k];
+    } else if (MODE != TREE_LDS16G) {
       float4* s_cl = reinterpret_cast<float4*>(s_tree + words);
       for (int k = threadIdx.x; k < S.num_clusters; k += TB) {
         s_cl[2 * k] = S.cl_lo[k];
@@ -615,6 +615,11 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
       else if (MODE == TREE_LDS16G)
         trace_phase<HYBRID, COUNT>(S, NodesDerived{s_tree}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
                                    S.num_materials, cnt, W, P);
+      else if (MODE == TREE_LDS16S)
+        trace_phase<HYBRID, COUNT>(
+            S, NodesDerived{s_tree},
+            ClustersSuper{s_tree + S.num_nodes, S.cl_lo, S.cl_hi, S.cl_n}, R, fastAABB,
+            S.num_materials, cnt, W, P);
       else if (MODE == TREE_PACKED)
         trace_phase<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
                                    S.num_materials, cnt, W, P);
@@ -1184,6 +1189,9 @@ struct ShadeLDS {
   uint32_t mats[STAGE ? STAGE_MATS * sizeof(DevMaterial) / 4 : 1];
 };
 
+// what a fused-shading workgroup needs beside a resident intersect workgroup (the LDS16S route leaves it free)
+constexpr size_t SHADE_LDS_RESERVE = sizeof(ShadeLDS<true, SHADE_TB>);
+
 // STAGE: the analytic geoms and the materials copied into LDS (small scenes: their per-lane reads, indexed
 // by hit and by nearest-first order, are then LDS reads instead of L2 round trips)
 // (SYNC false: the caller's next __syncthreads publishes the copy -- k_shade_fused overlaps it with the
@@ -1670,6 +1678,7 @@ struct kdpt_ctx {
   int full_trace_grid = 0;  // the occupancy-derived grid (trace_grid before a "trace_grid_frac" knob)
   bool grid_env = false;  // trace_grid fixed by the "trace_grid_frac" tuning knob
   bool force_global_tree = false;  // "tree_global" tuning knob: keep the tree in HBM/L2
+  bool super_cull = true;          // "super_cull" tuning knob: 0 = no TREE_LDS16S route (one-level cull)
   int tree_format = 0;             // "tree_format" knob: 16 / 32 = LDS node records of that size only
   size_t tree_lds = 0;    // dynamic LDS bytes of the intersect kernel (TREE_LDS)
   int* tile_counts = nullptr;
@@ -1901,15 +1910,31 @@ int drain_intersect_events(kdpt_ctx* c) {
   return KDPT_OK;
 }
 
+// Half-precision bits of the largest half <= x (half_down) / the smallest half >= x (half_up); overflow goes
+// to -inf / +inf, so the rounded value always bounds x (x finite).
+uint32_t half_down(float x) {
+  const _Float16 h0 = (_Float16)x;  // round to nearest
+  uint16_t b = __builtin_bit_cast(uint16_t, h0);
+  if ((float)h0 > x) {  // one step towards -inf
+    if (b == 0x0000u) b = 0x8001u;
+    else if (b & 0x8000u) b = (uint16_t)(b + 1u);
+    else b = (uint16_t)(b - 1u);
+  }
+  return b;
+}
+uint32_t half_up(float x) { return half_down(-x) ^ 0x8000u; }
+
 // Big leaves as clusters of <= 64 triangles (kdpt_device.h DevScene::leaf_cl ...): Morton order of
 // the triangle centroids inside the leaf's box, consecutive runs of 64, each with its exact float box.
 // Only the order in which the wave tests a big leaf's triangles changes; results are recombined by
 // original index, so any grouping is exact.
 int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>& tv, const std::vector<float4>& e1,
-                   const std::vector<float4>& e2, std::vector<int2>& leaf_cl) {
+                   const std::vector<float4>& e2, std::vector<int2>& leaf_cl, std::vector<int2>& leaf_sp) {
   const int nn = sc->num_nodes;
   leaf_cl.assign(nn, make_int2(0, 0));
-  std::vector<float4> lo, hi, cv0, ce1, ce2;
+  leaf_sp.assign(nn, make_int2(0, 0));
+  std::vector<int4> sp;  // super-clusters: SUPER consecutive clusters of one leaf (DevScene::sup)
+  std::vector<float4> lo, hi, nrm, cv0, ce1, ce2;
   std::vector<int2> info;
   auto spread = [](uint32_t v) {
     uint32_t r = 0;
@@ -1959,8 +1984,55 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
         ce1.push_back(make_float4(0.0f, 0.0f, 0.0f, ibits(-1)));
         ce2.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
       }
-      lo.push_back(make_float4(l[0], l[1], l[2], 0.0f));
-      hi.push_back(make_float4(h[0], h[1], h[2], 0.0f));
+      // the slab: n = the normalised sum of the triangles' (v1 - v0) x (v2 - v0), c as the kernel forms it,
+      // [min, max] of n . (v - c) over the vertices in double, rounded outward to float
+      const float cc[3] = {0.5f * (l[0] + h[0]), 0.5f * (l[1] + h[1]), 0.5f * (l[2] + h[2])};
+      double ns[3] = {0, 0, 0};
+      for (int k = b; k < b + cnt; k++) {
+        const kdpt_tri_bare& T = sc->tris[start + key[k].second];
+        const double ax = (double)T.x2 - T.x1, ay = (double)T.y2 - T.y1, az = (double)T.z2 - T.z1;
+        const double bx = (double)T.x3 - T.x1, by = (double)T.y3 - T.y1, bz = (double)T.z3 - T.z1;
+        ns[0] += ay * bz - az * by;
+        ns[1] += az * bx - ax * bz;
+        ns[2] += ax * by - ay * bx;
+      }
+      const double nl = std::sqrt(ns[0] * ns[0] + ns[1] * ns[1] + ns[2] * ns[2]);
+      float nf[3] = {0.0f, 0.0f, 0.0f};
+      float dlo = -FLT_MAXV, dhi = FLT_MAXV;
+      if (nl > 0 && std::isfinite(nl)) {
+        for (int a = 0; a < 3; a++) nf[a] = (float)(ns[a] / nl);
+        double mn = 1e300, mx = -1e300;
+        for (int k = b; k < b + cnt; k++) {
+          const kdpt_tri_bare& T = sc->tris[start + key[k].second];
+          const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
+          for (int v = 0; v < 3; v++) {
+            const double dv = (double)nf[0] * ((double)vx[v] - cc[0]) + (double)nf[1] * ((double)vy[v] - cc[1]) +
+                              (double)nf[2] * ((double)vz[v] - cc[2]);
+            mn = std::min(mn, dv);
+            mx = std::max(mx, dv);
+          }
+        }
+        dlo = std::nextafter((float)mn, -FLT_MAXV);
+        dhi = std::nextafter((float)mx, FLT_MAXV);
+      }
+      lo.push_back(make_float4(l[0], l[1], l[2], dlo));
+      hi.push_back(make_float4(h[0], h[1], h[2], dhi));
+      nrm.push_back(make_float4(nf[0], nf[1], nf[2], 0.0f));
+    }
+    const int c0 = leaf_cl[i].x, ncl = leaf_cl[i].y;
+    leaf_sp[i] = make_int2((int)sp.size(), (ncl + SUPER - 1) / SUPER);
+    for (int b = 0; b < ncl; b += SUPER) {
+      const int cnt = std::min(SUPER, ncl - b);
+      float4 sl = lo[c0 + b], sh = hi[c0 + b];
+      for (int k = c0 + b + 1; k < c0 + b + cnt; k++) {
+        sl.x = std::min(sl.x, lo[k].x); sl.y = std::min(sl.y, lo[k].y); sl.z = std::min(sl.z, lo[k].z);
+        sh.x = std::max(sh.x, hi[k].x); sh.y = std::max(sh.y, hi[k].y); sh.z = std::max(sh.z, hi[k].z);
+      }
+      // half precision rounded outward: the stored box holds the exact one
+      const uint32_t lx = half_down(sl.x), ly = half_down(sl.y), lz = half_down(sl.z);
+      const uint32_t hx = half_up(sh.x), hy = half_up(sh.y), hz = half_up(sh.z);
+      sp.push_back(make_int4((int)(lx | ly << 16), (int)(lz | hx << 16), (int)(hy | hz << 16),
+                             (int)((uint32_t)(c0 + b) << 5 | (uint32_t)(cnt - 1))));
     }
   }
   int2 *dl, *di;
@@ -1971,6 +2043,13 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
       (rc = dupload(c, &dv0, cv0.data(), cv0.size())) || (rc = dupload(c, &de1, ce1.data(), ce1.size())) ||
       (rc = dupload(c, &de2, ce2.data(), ce2.size())))
     return rc;
+  int4* dsp;
+  float4* dn;
+  if ((rc = dupload(c, &dsp, sp.data(), sp.size())) || (rc = dupload(c, &dn, nrm.data(), nrm.size()))) return rc;
+  c->S.cl_n = dn;
+  c->S.cl_slab = 1;
+  c->S.sup = dsp;
+  c->S.num_supers = (int)sp.size();
   c->S.leaf_cl = dl;
   c->S.num_clusters = (int)info.size();
   c->S.cl_info = di;
@@ -2097,6 +2176,10 @@ int setup_trace(kdpt_ctx* c) {
     if (c->S.dnodes && c->tree_format != 32) {
       const size_t t16 = 16 * (size_t)c->S.num_nodes, st16 = per_wave * (TRACE_BLOCK16 / 64);
       if (st16 + t16 + cl_bytes <= lds_max) cands.push_back({TREE_LDS16, t16 + cl_bytes});
+      // (leaving room for a fused-shading workgroup's LDS beside the intersect workgroup)
+      const size_t sp_bytes = 16 * (size_t)c->S.num_supers;
+      if (c->S.snodes && c->super_cull && st16 + t16 + sp_bytes + SHADE_LDS_RESERVE <= lds_max)
+        cands.push_back({TREE_LDS16S, t16 + sp_bytes});
       if (st16 + t16 <= lds_max) cands.push_back({TREE_LDS16G, t16});
     }
   }
@@ -2107,6 +2190,7 @@ int setup_trace(kdpt_ctx* c) {
     int b = 0;
     rc = k.mode == TREE_LDS16 ? trace_occupancy_all<TREE_LDS16>(c, k.lds, &b)
        : k.mode == TREE_LDS16G ? trace_occupancy_all<TREE_LDS16G>(c, k.lds, &b)
+       : k.mode == TREE_LDS16S ? trace_occupancy_all<TREE_LDS16S>(c, k.lds, &b)
                                 : trace_occupancy_all<TREE_LDS>(c, k.lds, &b);
     if (rc) return rc;
     const int waves = b * (k.mode == TREE_LDS ? TRACE_BLOCK : TRACE_BLOCK16) / 64;
@@ -2378,8 +2462,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
       return bail(rc);
     c->S.nodes = dnodes;
     c->S.pnodes = nullptr;
-    std::vector<int2> leaf_cl;
-    if ((rc = build_clusters(c, sc, tv, e1, e2, leaf_cl))) return bail(rc);
+    std::vector<int2> leaf_cl, leaf_sp;
+    if ((rc = build_clusters(c, sc, tv, e1, e2, leaf_cl, leaf_sp))) return bail(rc);
     std::vector<int4> packed;
     if (pack_nodes(sc->nodes, nn, leaf_cl, packed)) {
       int4* dp;
@@ -2387,10 +2471,16 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
       c->S.pnodes = dp;
     }
     c->S.dnodes = nullptr;
+    c->S.snodes = nullptr;
     if (pack_nodes16(sc->nodes, nn, leaf_cl, packed)) {
       int4* dp;
       if ((rc = dupload(c, &dp, packed.data(), packed.size()))) return bail(rc);
       c->S.dnodes = dp;
+      // the same records with a big leaf's first super-cluster (TREE_LDS16S), when the scene has supers
+      if (c->S.num_supers > 0 && pack_nodes16(sc->nodes, nn, leaf_sp, packed)) {
+        if ((rc = dupload(c, &dp, packed.data(), packed.size()))) return bail(rc);
+        c->S.snodes = dp;
+      }
     }
     c->S.tv0 = dtv;
     c->S.te1 = de1;
@@ -2579,10 +2669,15 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     if (!(value > 0.0 && value <= 1.0)) return fail(KDPT_ERR_ARG, "trace_grid_frac must be in (0, 1]");
     c->trace_grid = std::max(1, (int)(c->full_trace_grid * value));
     c->grid_env = value < 1.0;
-  } else if (k == "tree_format" || k == "tree_global") {
+  } else if (k == "tree_format" || k == "tree_global" || k == "super_cull" || k == "cluster_slab") {
     if (k == "tree_format") {
       if (v != 0 && v != 16 && v != 32) return fail(KDPT_ERR_ARG, "tree_format must be 0 (best), 16 or 32");
       c->tree_format = v;
+    } else if (k == "super_cull") {
+      c->super_cull = v != 0;
+    } else if (k == "cluster_slab") {
+      c->S.cl_slab = v != 0;
+      return KDPT_OK;
     } else {
       c->force_global_tree = v != 0;
     }
@@ -3113,6 +3208,8 @@ void launch_trace_mode(kdpt_ctx* c, const TraceArgs& a, hipStream_t st) {
     hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS16>), g, dim3(trace_block<TREE_LDS16>()), c->tree_lds, st, a);
   else if (c->tree_mode == TREE_LDS16G)
     hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS16G>), g, dim3(trace_block<TREE_LDS16G>()), c->tree_lds, st, a);
+  else if (c->tree_mode == TREE_LDS16S)
+    hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_LDS16S>), g, dim3(trace_block<TREE_LDS16S>()), c->tree_lds, st, a);
   else if (c->tree_mode == TREE_PACKED)
     hipLaunchKernelGGL((k_trace<HYBRID, COUNT, TREE_PACKED>), g, dim3(trace_block<TREE_PACKED>()), 0, st, a);
   else

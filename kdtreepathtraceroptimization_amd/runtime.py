@@ -469,7 +469,8 @@ class PathTracer:
         _check(self.lib.kdpt_count_iteration(self._ctx, int(iteration), out), "kdpt_count_iteration")
         return int(out[0]), int(out[1]), int(out[2])
 
-    TREE_MODES = {0: "hbm-64B", 1: "hbm-32B", 2: "lds-32B", 3: "lds-16B-derived", 4: "lds-16B-derived+hbm-clusters"}
+    TREE_MODES = {0: "hbm-64B", 1: "hbm-32B", 2: "lds-32B", 3: "lds-16B-derived", 4: "lds-16B-derived+hbm-clusters",
+                  5: "lds-16B-derived+supers"}
 
     def trace_config(self) -> dict:
         """kdpt_trace_config: where the intersect kernel reads the tree, its workgroup, grid and LDS."""
@@ -496,7 +497,7 @@ class PathTracer:
         keys = ("node_trips", "node_cycles", "big_sweeps", "big_cycles", "small_phases", "small_rounds",
                 "small_cycles", "final_cycles", "setup_cycles", "geom_cycles", "post_cycles", "node_lane_steps",
                 "big_leaves", "big_clusters", "big_pass", "big_multi", "small_pairs", "node_leafwait_steps",
-                "node_done_steps", "tail_cycles", "tail_node_done_steps",
+                "node_done_steps", "tail_cycles", "tail_node_done_steps", "big_supers", "big_cull_cycles",
                 "chunks", "chunk_cycles", "aabb", "tri", "hit")
         prof = dict(zip(keys, (int(out[k]) for k in range(len(keys)))))
         k0 = len(keys)

@@ -28,7 +28,7 @@ def _report():
 
 # kernel name fragment -> minimum waves per SIMD
 HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_traceILb1ELb0ELi4E": 4, "k_traceILb0ELb0ELi4E": 4,
-       "k_shade_fused": 6, "k_geoms": 4, "k_gen_rays": 4}
+       "k_traceILb1ELb0ELi5E": 4, "k_traceILb0ELb0ELi5E": 4, "k_shade_fused": 6, "k_geoms": 4, "k_gen_rays": 4}
 
 
 # k_trace is compiled for 5 waves per SIMD (96 VGPRs) so that a shading wave of another batch fits beside its
@@ -39,8 +39,10 @@ HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_traceILb1ELb0ELi
 # The derived-box route (NodesDerived, the C5 icosphere's tree in LDS) keeps the current node's box in 6 more
 # registers at the same 96-VGPR cap; its spills are the price of the tree in LDS (+10.6 % on C5, and a 4-wave
 # cap without spills measured 8 % slower; profiles/r03_ab_log.md)
+# The two-level cull route (TREE_LDS16S, the C5 icosphere) adds the super pass's survivor bookkeeping on top.
 SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 32, "k_traceILb0ELb0ELi2E": 32, "k_traceILb1ELb0ELi4E": 80,
-              "k_traceILb0ELb0ELi4E": 80, "k_shade_fused": 20}
+              "k_traceILb0ELb0ELi4E": 80, "k_traceILb1ELb0ELi5E": 100, "k_traceILb0ELb0ELi5E": 100,
+              "k_shade_fused": 20}
 
 
 @pytest.mark.parametrize("frag", sorted(HOT))

@@ -82,15 +82,18 @@ def test_icosphere_bit_exact_vs_oracle(kdpt, oracle, level, res, depth, cap, ite
 
 
 @pytest.mark.gpu
-def test_c5_full_size_bit_exact_vs_oracle_pin(kdpt):
+@pytest.mark.parametrize("super_cull,route", [(1, "lds-16B-derived+supers"), (0, "lds-16B-derived+hbm-clusters")])
+def test_c5_full_size_bit_exact_vs_oracle_pin(kdpt, super_cull, route):
     """One full C5 iteration (1600x1600, depth 16, cap 16, 1.31 M triangles) equals the oracle's render
-    committed in c5_anchor.json: sha256 of the float32 image, segments, and the live paths per bounce."""
+    committed in c5_anchor.json: sha256 of the float32 image, segments, and the live paths per bounce; on the
+    default route (two-level cluster cull) and the one-level route."""
     from conftest import TESTS
     pin = json.load(open(os.path.join(TESTS, "golden", "c5_anchor.json")))
     desc = load_fixture_scene(pin["scene"], pin["mesh"], res=tuple(pin["res"]), depth=pin["depth"])
     with kdpt.PathTracer(kdpt.SceneData.from_description(desc), kdpt.default_options(bounce_cap=pin["bounce_cap"]),
                          device=0) as pt:
-        assert pt.trace_config()["tree"] == "lds-16B-derived+hbm-clusters"
+        pt.set_tuning("super_cull", super_cull)
+        assert pt.trace_config()["tree"] == route
         pt.trace_iteration(pin["iter"])
         st = pt.stats()
         img = pt.image()
