@@ -26,8 +26,9 @@ def libm_diff():
     os.makedirs(os.path.dirname(exe), exist_ok=True)
     subprocess.run(["g++", "-O2", "-std=c++17", "-fopenmp", "-ffp-contract=off", "-fno-fast-math",
                     "-fno-builtin-sin", "-fno-builtin-cos", "-fno-builtin-sinf", "-fno-builtin-cosf",
-                    "-include", "omp.h", os.path.join(ROOT, "tests", "native", "libm_diff.cpp"), "-o", exe, "-lm"],
+                    "-include", "omp.h", os.path.join(ROOT, "tests", "native", "libm_diff.cpp"), "-o", exe + f".{os.getpid()}", "-lm"],
                    check=True)
+    os.replace(exe + f".{os.getpid()}", exe)  # parallel workers may be running the old one
     return exe
 
 

@@ -52,10 +52,14 @@ MALFORMED_SCENES = {
 def asan_host():
     exe = os.path.join(ROOT, "build", "asan_host")
     os.makedirs(os.path.dirname(exe), exist_ok=True)
+    # built under a per-process name and renamed into place: parallel test workers (pytest -n) may be running
+    # the previous binary
+    tmp = f"{exe}.{os.getpid()}"
     subprocess.run(["g++", *SAN, "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-I", os.path.join(ROOT, "include"),
                     os.path.join(TESTS, "native", "asan_host.cpp"), os.path.join(TESTS, "native", "no_device_build.cpp"),
                     os.path.join(CSRC, "scene_host.cpp"),
-                    os.path.join(CSRC, "image_io.cpp"), "-o", exe], check=True)
+                    os.path.join(CSRC, "image_io.cpp"), "-o", tmp], check=True)
+    os.replace(tmp, exe)
     return exe
 
 
@@ -104,7 +108,8 @@ def test_oracle_and_traversal_clean_under_sanitizers():
     exe = os.path.join(ROOT, "build", "traverse_diff_asan")
     subprocess.run(["g++", *SAN, "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-fopenmp", "-I",
                     os.path.join(ROOT, "include"), "-x", "c++", os.path.join(TESTS, "native", "traverse_diff.cpp"),
-                    "-x", "c", os.path.join(ROOT, "oracle", "kdpt_oracle.c"), "-o", exe, "-lm"], check=True)
+                    "-x", "c", os.path.join(ROOT, "oracle", "kdpt_oracle.c"), "-o", exe + f".{os.getpid()}", "-lm"], check=True)
+    os.replace(exe + f".{os.getpid()}", exe)
     for mesh in ("sphere_low_1", "dragon_5"):
         for hybrid in ("1", "0"):
             p = subprocess.run([exe, f"{REFERENCE}/scenes/cornell.txt", f"{REFERENCE}/scenes/{mesh}.obj", "3000",

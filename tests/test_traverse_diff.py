@@ -19,7 +19,8 @@ def traverse_diff(oracle):
     os.makedirs(os.path.dirname(exe), exist_ok=True)
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-I", os.path.join(REPO, "include"),
                     os.path.join(REPO, "tests", "native", "traverse_diff.cpp"), "-L", os.path.join(REPO, "oracle"),
-                    "-loracle", "-Wl,-rpath," + os.path.join(REPO, "oracle"), "-o", exe], check=True)
+                    "-loracle", "-Wl,-rpath," + os.path.join(REPO, "oracle"), "-o", exe + f".{os.getpid()}"], check=True)
+    os.replace(exe + f".{os.getpid()}", exe)  # parallel workers may be running the old one
     return exe
 
 
