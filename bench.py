@@ -68,6 +68,9 @@ def parse():
     ap.add_argument("--pipeline", type=int, default=8,
                     help="batches in flight (kdpt_trace_iterations; bit-identical to one at a time)")
     ap.add_argument("--batch", type=int, default=4, help="iterations sharing each intersect launch (<= 4)")
+    ap.add_argument("--force-dist", action="store_true",
+                    help="run the process-group path (barriers, the in-timed-region reduce, stat all-reduces) even "
+                         "with one rank, e.g. to exercise RCCL on a one-GPU box")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="nccl = RCCL over xGMI (one GPU per rank); gloo = host-side reduce, for rehearsing the "
                          "N > 1 path with several ranks sharing one GPU")
@@ -193,7 +196,7 @@ def main():
     ndev = max(1, torch.cuda.device_count())
     local = local % ndev if args.dist_backend == "gloo" else local  # gloo rehearsal: ranks may share a GPU
     torch.cuda.set_device(local)
-    if world > 1:
+    if world > 1 or args.force_dist:
         import torch.distributed as dist
         if args.dist_backend == "nccl":
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))

@@ -1649,6 +1649,7 @@ __global__ void k_selftest_fresnel(const float* c, int n, float R0, float* f) {
 struct kdpt_ctx {
   int device = 0;
   hipStream_t stream = nullptr;
+  bool owns_stream = true;  // false: a pipeline group member, running on its group leader's stream
   kdpt_options opt{};
   kdpt_camera cam{};
   int traceDepth = 0;
@@ -1831,7 +1832,14 @@ int alloc_iteration_events(kdpt_ctx* c) {
 
 // A pipeline slot: shares p's scene upload and counters, owns its iteration buffers, its stream
 // and a partial image that k_gen_rays' iteration accumulates into.
-int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
+// Pipeline slots, members before their group leader (the leader owns the stream they share).
+void destroy_slots(kdpt_ctx* c) {
+  for (size_t k = c->slots.size(); k-- > 0;) kdpt_destroy(c->slots[k]);
+}
+
+// share: the stream of the slot's group leader (a group's batches all run on the leader's stream), or null
+// for a leader, which creates its own
+int make_slot(kdpt_ctx* p, kdpt_ctx** out, hipStream_t share = nullptr) {
   kdpt_ctx* c = new kdpt_ctx();
   c->parent = p;
   c->device = p->device;
@@ -1866,7 +1874,10 @@ int make_slot(kdpt_ctx* p, kdpt_ctx** out) {
   c->chunk_lo = p->chunk_lo;
   c->chunk_hi = p->chunk_hi;
   int rc;
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  if (share) {
+    c->stream = share;
+    c->owns_stream = false;
+  } else if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
     kdpt_destroy(c);
     return fail(KDPT_ERR_HIP, "hipStreamCreate failed");
   }
@@ -2644,7 +2655,7 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
   if (!c->slots.empty()) {
     int rc = kdpt_synchronize(c);
     if (rc) return rc;
-    for (auto sl : c->slots) kdpt_destroy(sl);
+    destroy_slots(c);
     for (auto e : c->slot_done) (void)hipEventDestroy(e);
     for (auto e : c->slot_free) (void)hipEventDestroy(e);
     c->slots.clear();
@@ -2783,7 +2794,7 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
     if (!c->slots.empty()) {
       int rc = kdpt_synchronize(c);
       if (rc) return rc;
-      for (auto sl : c->slots) kdpt_destroy(sl);
+      destroy_slots(c);
       for (auto e : c->slot_done) (void)hipEventDestroy(e);
       for (auto e : c->slot_free) (void)hipEventDestroy(e);
       c->slots.clear();
@@ -2791,9 +2802,13 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
       c->slot_free.clear();
     }
     c->slot_batch = B;
+    // Only the group leaders create streams, one after another: HIP maps streams onto its hardware queues
+    // (GPU_MAX_HW_QUEUES) in creation order, reusing the least-used queue once all exist, so a stream per
+    // slot context (8 x 4) had put pairs of leaders -- two batches' chains -- on one in-order queue.
     while ((int)c->slots.size() < depth * B) {
       kdpt_ctx* sl = nullptr;
-      int rc = make_slot(c, &sl);
+      const bool leader = c->slots.size() % B == 0;
+      int rc = make_slot(c, &sl, leader ? nullptr : c->slots[c->slots.size() / B * B]->stream);
       if (rc) return rc;
       c->slots.push_back(sl);
     }
@@ -2977,7 +2992,7 @@ int kdpt_destroy(kdpt_ctx* c) {
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
   if (c->accum_stream) (void)hipStreamSynchronize(c->accum_stream);
-  for (auto s : c->slots) kdpt_destroy(s);
+  destroy_slots(c);
   for (auto e : c->slot_done) (void)hipEventDestroy(e);
   for (auto e : c->slot_free) (void)hipEventDestroy(e);
   for (auto& evs : c->pending_ev)
@@ -2992,7 +3007,7 @@ int kdpt_destroy(kdpt_ctx* c) {
   if (c->ev1) (void)hipEventDestroy(c->ev1);
   for (auto e : c->bounce_ev)
     if (e) (void)hipEventDestroy(e);
-  if (c->stream) (void)hipStreamDestroy(c->stream);
+  if (c->stream && c->owns_stream) (void)hipStreamDestroy(c->stream);
   delete c;
   return KDPT_OK;
 }

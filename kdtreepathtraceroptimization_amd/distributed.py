@@ -25,8 +25,9 @@ def reduce_image(image, dist, dst: int = 0):
     With the "nccl" backend (RCCL) the device buffer is reduced in place over xGMI.  The "gloo" backend
     (CPU rehearsals, and several ranks sharing one GPU, which RCCL refuses) reduces a host copy, which
     is written back into the device buffer on `dst`."""
-    if dist is None or not dist.is_initialized() or dist.get_world_size() < 2:
+    if dist is None or not dist.is_initialized():
         return image
+    # (one rank: the reduce is a no-op that still runs through the backend, e.g. bench.py --force-dist)
     if image.is_cuda and dist.get_backend() == "gloo":
         host = image.cpu()
         dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM)
