@@ -39,9 +39,11 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # kdpt_trace_iterations keeps `--pipeline` batches in flight on their own HIP streams plus one accumulation
 # stream; HIP's default of 4 hardware queues per process would make some of them share a queue (and
-# serialise), so ask for 16 (<= 32) before the runtime initialises.
-if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 16:
-    os.environ["GPU_MAX_HW_QUEUES"] = "16"
+# serialise), so ask for 24 (<= 32) before the runtime initialises: 12 batch streams, the context's, the
+# accumulation and torch's, and the queues an RCCL communicator takes (multi-GPU runs) all get their own
+# (16 queues under RCCL: 4687 against 5695 Mrays/s, profiles/r03_ab_log.md).
+if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
+    os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
 METRIC = json.load(open(os.path.join(ROOT, "BASELINE.json")))["metric"]
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
@@ -65,7 +67,7 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=3, help="CPU-baseline repeats (median and spread)")
     ap.add_argument("--cpu-iters", type=int, default=8, help="iterations per repeat of the multi-thread CPU leg")
-    ap.add_argument("--pipeline", type=int, default=8,
+    ap.add_argument("--pipeline", type=int, default=12,
                     help="batches in flight (kdpt_trace_iterations; bit-identical to one at a time)")
     ap.add_argument("--batch", type=int, default=4, help="iterations sharing each intersect launch (<= 4)")
     ap.add_argument("--force-dist", action="store_true",
@@ -278,6 +280,13 @@ def main():
         "rays_per_launch": round(rays_per_launch, 1),
         "k_trace_ms_per_step": round(kernel_ms / max(1, args.steps * world), 4),
         "k_trace_busy_share": round(kernel_ms * share / (dt * 1e3 * world), 4),
+        # every k_trace instruction of the timed region over its wall time and the whole chip: a lower bound on
+        # the kernel's issue rate that does not depend on launch spans (with more launches in flight than grid
+        # shares, busy share > 1, a launch's span includes waiting for CUs the other launches hold)
+        "chip_wide_achieved": (round(roof["valu_per_ray"] * rays / (dt * world) / 1e9, 2)
+                               if roof.get("valu_per_ray") else None),
+        "chip_wide_frac": (round(roof["valu_per_ray"] * rays / (dt * world) / 1e9 / VALU_PEAK_GINST, 4)
+                           if roof.get("valu_per_ray") else None),
         "algorithmic": {"bytes_per_ray": round(alg_bytes / max(1, cand), 1),
                         "GBps_per_launch": round(alg_bytes / max(1, cand) * rays_per_launch / (avg_launch_ms * 1e-3)
                                                  / 1e9, 1) if avg_launch_ms > 0 else None,

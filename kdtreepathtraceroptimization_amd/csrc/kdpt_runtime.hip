@@ -2823,10 +2823,12 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
   }
   const int ngroups = (int)c->slot_done.size();
   // With several batches in flight each intersect launch gets a share of the chip (2/depth of the
-  // persistent grid, all of it for depth <= 2): a launch's length is set by its heaviest rays, so
-  // concurrent launches on disjoint CU subsets overlap those tails instead of queueing behind them.
+  // persistent grid, all of it for depth <= 2, a quarter from depth 8 on): a launch's length is set by its
+  // heaviest rays, so concurrent launches on disjoint CU subsets overlap those tails instead of queueing
+  // behind them.  (Sweep with every batch on its own hardware queue: a quarter is best at depths 8-12.)
   for (auto sl : c->slots)
-    sl->trace_grid = c->grid_env ? c->trace_grid : std::max(1, c->trace_grid * 2 / std::max(2, depth));
+    sl->trace_grid =
+        c->grid_env ? c->trace_grid : std::max(1, c->trace_grid * 2 / std::min(8, std::max(2, depth)));
   c->stats.intersect_grid_share =
       c->slots.empty() ? 1.0f : (float)c->slots[0]->trace_grid / (float)std::max(1, c->full_trace_grid);
   // diagnostic ("profile_batches" knob): the counting intersect kernel (kdpt_wave_profile after sync)
