@@ -39,9 +39,9 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 # kdpt_trace_iterations keeps `--pipeline` batches in flight on their own HIP streams plus one accumulation
 # stream; HIP's default of 4 hardware queues per process would make some of them share a queue (and
-# serialise), so ask for 24 (<= 32) before the runtime initialises: 12 batch streams, the context's, the
+# serialise), so ask for 24 (<= 32) before the runtime initialises: the batch streams, the context's, the
 # accumulation and torch's, and the queues an RCCL communicator takes (multi-GPU runs) all get their own
-# (16 queues under RCCL: 4687 against 5695 Mrays/s, profiles/r03_ab_log.md).
+# (16 queues under RCCL at 12 batches: 4687 against 5695 Mrays/s, profiles/r03_ab_log.md).
 if int(os.environ.get("GPU_MAX_HW_QUEUES", "4") or 4) < 24:
     os.environ["GPU_MAX_HW_QUEUES"] = "24"
 
@@ -67,9 +67,9 @@ def parse():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-repeats", type=int, default=3, help="CPU-baseline repeats (median and spread)")
     ap.add_argument("--cpu-iters", type=int, default=8, help="iterations per repeat of the multi-thread CPU leg")
-    ap.add_argument("--pipeline", type=int, default=12,
+    ap.add_argument("--pipeline", type=int, default=8,
                     help="batches in flight (kdpt_trace_iterations; bit-identical to one at a time)")
-    ap.add_argument("--batch", type=int, default=4, help="iterations sharing each intersect launch (<= 4)")
+    ap.add_argument("--batch", type=int, default=8, help="iterations sharing each intersect launch (<= 8)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the process-group path (barriers, the in-timed-region reduce, stat all-reduces) even "
                          "with one rank, e.g. to exercise RCCL on a one-GPU box")

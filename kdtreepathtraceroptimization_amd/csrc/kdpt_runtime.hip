@@ -196,7 +196,7 @@ constexpr int trace_block() { return MODE == 2 ? TRACE_BLOCK : (MODE >= 3 ? TRAC
 // Up to MAXB iterations (each its own path buffers) at the same bounce share one intersect launch:
 // more rays per launch keep the lanes of the persistent waves busy.
 #ifndef KDPT_MAXB
-#define KDPT_MAXB 4  // tools/build_variant.sh experiments only
+#define KDPT_MAXB 8  // tools/build_variant.sh experiments only
 #endif
 constexpr int MAXB = KDPT_MAXB;
 struct TraceIter {

@@ -40,8 +40,9 @@ HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_traceILb1ELb0ELi
 # registers at the same 96-VGPR cap; its spills are the price of the tree in LDS (+10.6 % on C5, and a 4-wave
 # cap without spills measured 8 % slower; profiles/r03_ab_log.md)
 # The two-level cull route (TREE_LDS16S, the C5 icosphere) adds the super pass's survivor bookkeeping on top.
-SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 32, "k_traceILb0ELb0ELi2E": 32, "k_traceILb1ELb0ELi4E": 80,
-              "k_traceILb0ELb0ELi4E": 80, "k_traceILb1ELb0ELi5E": 100, "k_traceILb0ELb0ELi5E": 100,
+# Batches of up to 8 iterations per intersect launch (MAXB) cost the derived-box routes a few more bytes.
+SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 32, "k_traceILb0ELb0ELi2E": 32, "k_traceILb1ELb0ELi4E": 88,
+              "k_traceILb0ELb0ELi4E": 88, "k_traceILb1ELb0ELi5E": 100, "k_traceILb0ELb0ELi5E": 100,
               "k_shade_fused": 20}
 
 

@@ -259,7 +259,7 @@ def test_pbo_into_device_memory(kdpt):
         assert np.array_equal(dev.cpu().numpy(), host)
 
 
-@pytest.mark.parametrize("pipeline,batch", [(1, 1), (3, 1), (2, 3), (1, 4), (8, 4), (5, 2), (12, 4)])
+@pytest.mark.parametrize("pipeline,batch", [(1, 1), (3, 1), (2, 3), (1, 4), (8, 4), (5, 2), (12, 4), (3, 8), (8, 8), (2, 5)])
 def test_pipelined_iterations_bit_exact(kdpt, pipeline, batch):
     """kdpt_trace_iterations (batches sharing intersect launches, several batches in flight, partial
     images added in order) gives the same image bits and segment counts as one kdpt_trace_iteration
