@@ -3,17 +3,19 @@
 Metric (BASELINE.json): Mrays/s at 800x800, depth 8, cornell + dragon (dragon_5.obj: the only dragon mesh
 present -- cornell9.txt does not exist), plus ms per iteration.
 
-A step is one frame of `--spp-per-step` samples per pixel (default 256): that many iterations of the whole
-hot path (camera rays -> up to 8 x [intersect + KD traversal + scatter + shade + gather + stable
-compaction]), each a distinct global iteration number (its own RNG seed).  Mrays/s = path segments
-launched into the intersect stage, summed over all ranks, / the max-over-ranks wall time of the K timed
-steps.  Iterations stay in flight across the frame (kdpt_trace_iterations), so the GPU stays at steady
-state; `ms_per_iteration` is reported beside `ms_per_step`.  256 samples per step make the driver's
-`--steps 20 --warmup 5` timed region about 2.5 s of GPU work (5 120 iterations).
+A step is one frame (kdpt_render_frames): `--spp-per-step` samples per pixel per GPU (default 1024, weak
+scaling) or a fixed `--total-spp` split over the GPUs (strong scaling, C4's "256 spp sharded 32/GPU").  A
+sample is one iteration of the whole hot path (camera rays -> up to 8 x [intersect + KD traversal + scatter +
+shade + gather + stable compaction]) with its own global iteration number (RNG seed).  Frames stay in flight
+back to back (frame f + 1 renders while frame f is reduced), so the GPU stays at steady state.  Mrays/s =
+path segments launched into the intersect stage, summed over all ranks, / the max-over-ranks wall time of
+the K timed frames; `ms_per_iteration` is reported beside `ms_per_step`.  The driver's `--steps 20 --warmup 5`
+times 20 480 iterations (about 8.5 s of GPU work for C3).
 
-Multi-GPU (one process per GPU, `torch.distributed.run`): samples per pixel shard across ranks (rank r
-renders global iterations r+1, r+1+N, ...: weak scaling) and the float3 accumulation images are summed on
-rank 0 with one RCCL reduce over xGMI inside the timed region.
+Multi-GPU (one process per GPU, `torch.distributed.run`): rank r renders the frame's global iterations
+f*F + 1 + r, stride N, and each frame's float3 image is summed on rank 0 by one RCCL ncclReduce issued inside
+libkdpt (kdpt_comm_init / kdpt_render_frames; the communicator's unique id goes out over the process group).
+The gloo backend (ranks sharing a GPU, CPU rehearsals) hands each rank's frame shares out and reduces them here.
 
 Roofline: the dominant kernel is k_trace (the KD traversal of the rays that meet the KD root box).  It is
 bound by VALU issue and latency, not HBM (its tree lives in LDS, its triangles in L2), so the
@@ -56,7 +58,11 @@ def parse():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=2)
-    ap.add_argument("--spp-per-step", type=int, default=256, help="iterations (samples per pixel) per step")
+    ap.add_argument("--spp-per-step", type=int, default=1024,
+                    help="weak scaling (default): samples per pixel per GPU in each step's frame")
+    ap.add_argument("--total-spp", type=int, default=None,
+                    help="strong scaling: samples per pixel of each step's frame, split over the GPUs "
+                         "(C4: 256, 32 per GPU on 8)")
     ap.add_argument("--mesh", default="dragon_5")
     ap.add_argument("--scene", default="cornell")
     ap.add_argument("--res", type=int, nargs=2, default=(800, 800))
@@ -69,7 +75,7 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=8, help="iterations per repeat of the multi-thread CPU leg")
     ap.add_argument("--pipeline", type=int, default=8,
                     help="batches in flight (kdpt_trace_iterations; bit-identical to one at a time)")
-    ap.add_argument("--batch", type=int, default=8, help="iterations sharing each intersect launch (<= 8)")
+    ap.add_argument("--batch", type=int, default=8, help="iterations sharing each intersect launch (<= MAXB)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the process-group path (barriers, the in-timed-region reduce, stat all-reduces) even "
                          "with one rank, e.g. to exercise RCCL on a one-GPU box")
@@ -78,8 +84,8 @@ def parse():
                          "N > 1 path with several ranks sharing one GPU")
     ap.add_argument("--tune", action="append", default=[], metavar="NAME=VALUE",
                     help="kdpt_set_tuning knob for A/B runs (not for reported numbers)")
-    ap.add_argument("--dump-image", default=None, help="rank 0 saves the reduced float3 image of the timed "
-                    "iterations here (.npy; tests/test_gpu_sharded.py checks the N > 1 path with it)")
+    ap.add_argument("--dump-image", default=None, help="rank 0 saves the sum of the timed frames' reduced float3 "
+                    "images here (.npy; tests/test_gpu_sharded.py checks the N > 1 path with it)")
     ap.add_argument("--pmc-profile", default=None, help="profile JSON for the VALU roofline (default: "
                     "profiles/pmc_<scene>_<mesh>_<W>x<H>.json)")
     return ap.parse_args()
@@ -205,42 +211,59 @@ def main():
         else:
             dist.init_process_group("gloo")
     from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options, load_fixture_scene
-    from kdtreepathtraceroptimization_amd.distributed import global_iteration, reduce_image
+    from kdtreepathtraceroptimization_amd.distributed import frame_share
+    from kdtreepathtraceroptimization_amd.runtime import comm_unique_id
 
-    S = max(1, args.spp_per_step)
+    # a step is one frame: weak scaling renders spp-per-step samples per GPU per frame, strong scaling a fixed
+    # --total-spp per frame split over the GPUs
+    strong = args.total_spp is not None
+    F = max(1, args.total_spp if strong else args.spp_per_step * world)  # global iterations per frame
     desc = load_fixture_scene(args.scene, args.mesh, res=tuple(args.res), depth=args.depth)
     sd = SceneData.from_description(desc)
     W, H = sd.resolution
-    accum = torch.zeros(3 * W * H, dtype=torch.float32, device=f"cuda:{local}")
-    opt = default_options(testing_mode=1, short_stack=0 if args.bare else 1, external_image=accum.data_ptr(),
-                          bounce_cap=args.bounce_cap)
+    opt = default_options(testing_mode=1, short_stack=0 if args.bare else 1, bounce_cap=args.bounce_cap)
     pt = PathTracer(sd, opt, device=local)
     for kv in args.tune:
         name, val = kv.split("=", 1)
         pt.set_tuning(name, float(val))
+    # the framebuffer reduce: RCCL inside the library (kdpt_comm_init: rank 0's unique id handed out through
+    # the process group), or -- gloo rehearsals, ranks sharing a GPU -- each rank's frame shares handed out
+    # and reduced here over gloo
+    gloo = dist is not None and args.dist_backend == "gloo"
+    if dist is not None:
+        if gloo:
+            pt.comm_init(world, rank, None)
+        else:
+            ids = [comm_unique_id() if rank == 0 else None]
+            dist.broadcast_object_list(ids, src=0)
+            pt.comm_init(world, rank, ids[0])
 
-    def first_iter(local_iteration):  # 1-based global iteration of this rank's local iteration j (spp sharding)
-        return global_iteration(local_iteration, world, rank)
-
-    # warmup: iterations disjoint from the timed ones (iteration 2's extra sort lands here)
+    # warmup: frames disjoint from the timed ones (iteration 2's extra sort lands here)
+    shares = torch.empty((args.steps, 3 * W * H), dtype=torch.float32, device=f"cuda:{local}") if gloo else None
     if args.warmup:
-        pt.trace_iterations(first_iter(0), args.warmup * S, stride=world, pipeline=args.pipeline, batch=args.batch)
+        pt.render_frames(0, args.warmup, F, pipeline=args.pipeline, batch=args.batch)
         pt.synchronize()
     # per-segment work counters from one untimed counting iteration of the timed range (informational)
-    aabb, tri, hit = pt.count_iteration(first_iter(args.warmup * S))
+    first_timed, _ = frame_share(args.warmup, F, world, rank)
+    aabb, tri, hit = pt.count_iteration(first_timed)
     aabb_prep, cand = pt.count_split()
     cnt_stats = pt.stats()
-    accum.zero_()
-    torch.cuda.synchronize()
+    pt.reset()  # zero image and totals: the timed frames alone
     st0 = pt.stats()
+    image = torch.zeros(3 * W * H, dtype=torch.float32) if gloo and rank == 0 else None
     if dist:
         dist.barrier()
     torch.cuda.synchronize()
     t0 = time.perf_counter()
-    pt.trace_iterations(first_iter(args.warmup * S), args.steps * S, stride=world, pipeline=args.pipeline,
-                        batch=args.batch)
-    pt.synchronize()
-    reduce_image(accum, dist)  # spp shards -> one framebuffer (the only exchange step)
+    pt.render_frames(args.warmup, args.steps, F, pipeline=args.pipeline, batch=args.batch,
+                     out=shares.data_ptr() if gloo else None)
+    pt.synchronize()  # (RCCL: every frame's reduce included)
+    if gloo:  # the same per-frame reduce over gloo, rank 0 adding the frames in order
+        for k in range(args.steps):
+            host = shares[k].cpu()
+            dist.reduce(host, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                image += host
     torch.cuda.synchronize()
     if dist:
         dist.barrier()
@@ -262,13 +285,13 @@ def main():
         seg, rays, kernel_ms, launches = int(tsum[0]), int(tsum[1]), float(tsum[2]), int(tsum[3])
     if rank == 0 and args.dump_image:
         import numpy as np
-        np.save(args.dump_image, accum.cpu().numpy())
+        np.save(args.dump_image, image.numpy() if gloo else pt.image().reshape(-1))
     if rank != 0:
         pt.close()
         if dist:
             dist.destroy_process_group()
         return
-    iters = args.steps * S * world
+    iters = args.steps * F
     avg_launch_ms = kernel_ms / max(1, launches)
     rays_per_launch = rays / max(1, launches)
     share = pt.trace_grid_share()
@@ -296,6 +319,7 @@ def main():
                                "hit": round(hit / count_seg, 5), "aabb_before_k_trace": round(aabb_prep / count_seg, 4),
                                "k_trace_share": round(cand / count_seg, 4)},
     })
+    per_gpu = F / world
     out = {
         "metric": METRIC,
         "value": round(seg / dt / 1e6, 3),
@@ -305,22 +329,24 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(dt * 1e3 / args.steps, 4),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": "f32",
         "data": f"synthetic camera rays over the reference's own scene assets ({args.scene}.txt + {args.mesh}.obj, "
                 "parsed fixtures under tests/golden); deterministic RNG seeded by global iteration",
         "config": {"workload": f"{args.scene}.txt + {args.mesh}.obj, {W}x{H}, depth {args.depth}, "
-                               f"bounce cap {args.bounce_cap}, {S} spp per step per GPU "
-                               f"({args.pipeline} x {args.batch} iterations in flight), "
+                               f"bounce cap {args.bounce_cap}, one {F}-spp frame per step"
+                               + (f" ({per_gpu:g} spp per GPU)" if world > 1 else "")
+                               + f", {args.pipeline} x {args.batch} iterations in flight, "
                                + ("short-stack hybrid KD traversal" if not args.bare else "bare traversal"),
                    "scene": args.scene, "mesh": args.mesh, "resolution": [W, H], "depth": args.depth,
-                   "bounce_cap": args.bounce_cap, "spp_per_step": S,
+                   "bounce_cap": args.bounce_cap, "spp_per_frame": F, "spp_per_gpu_per_frame": per_gpu,
                    "kd_nodes": sd.view.num_nodes, "kd_tri_refs": sd.view.num_tris,
                    "intersect": pt.trace_config(),
                    **({"tuning": args.tune} if args.tune else {}),
-                   "parallelism": (f"spp-sharded x{world} + " + ("RCCL reduce" if args.dist_backend == "nccl" else
-                                                                 "gloo host reduce (ranks sharing GPUs)"))
+                   "parallelism": (f"spp-sharded x{world}, one framebuffer reduce per frame: "
+                                   + ("RCCL ncclReduce inside libkdpt (kdpt_render_frames)"
+                                      if args.dist_backend == "nccl" else "gloo host reduce (ranks sharing GPUs)"))
                    if world > 1 else "single GPU"},
         "ms_per_iteration": round(dt * 1e3 * world / iters, 4),
         "segments_per_iteration": round(seg / iters, 1),

@@ -234,12 +234,52 @@ int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
  * per-ray node-step histogram),
  * "shade_batch" (1; 0 = one k_shade_fused launch per iteration instead of one per batch), "gen_geoms" (1;
  * 0 = camera rays and bounce 0's k_geoms as two launches instead of one k_gen_geoms_b),
+ * "tree_format" (0 = best fit; 16 / 32 = only that LDS record size), "super_cull" (1; 0 = no two-level
+ * super-cluster route), "cluster_slab" (1; 0 = no normal slab in the second cull level),
+ * "cluster_cull" (1; 0 = no cluster / chunk cull at all: every big-leaf cluster is swept, exact by
+ * construction), "cull_margin" (0 = the scene's; > 0 overrides the cull's margin coefficient),
  * "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots (they are remade). */
 int kdpt_set_tuning(kdpt_ctx *ctx, const char *name, double value);
 /* The intersect kernel's configuration: tree source (0 HBM 64-byte records, 1 HBM 32-byte, 2 LDS 32-byte,
- * 3 LDS 16-byte derived-box records + cluster boxes, 4 LDS 16-byte records with cluster boxes in HBM),
- * workgroup size, persistent grid (workgroups of the full grid) and dynamic LDS bytes per workgroup. */
+ * 3 LDS 16-byte derived-box records + cluster boxes, 4 LDS 16-byte records with cluster boxes in HBM,
+ * 5 LDS 16-byte records + super-cluster records (half-precision boxes rounded outward; cluster boxes and
+ * normal slabs in HBM, culled in two levels)), workgroup size, persistent grid (workgroups of the full grid)
+ * and dynamic LDS bytes per workgroup. */
 int kdpt_trace_config(kdpt_ctx *ctx, int *tree_mode, int *block, int *grid, long long *lds_bytes);
+/* The big-leaf cluster cull (and the brute-force chunk cull): the margin coefficient in use, the scene's
+ * rigorous coefficient, and exact = 1 when the one in use is >= the rigorous one -- the cull then never
+ * drops a cluster holding a triangle that passes glm's u/v tests, for any ray ("Cluster cull").
+ * exact = 0: the scene's triangles are too large for a rigorous margin that still culls; the cull is then
+ * conservative except for rays nearly coplanar with a triangle (tuning "cluster_cull" = 0 removes it). */
+int kdpt_cull_margin(kdpt_ctx *ctx, float *margin, double *rigorous, int *exact);
+
+/* ---- Multi-GPU: samples per pixel sharded across GPUs ----
+ * Frame f covers global iterations f*spp + 1 .. (f+1)*spp (the RNG seeds, iteration 2's sort and cacherays
+ * use these numbers); rank r of N renders those with (iteration - 1 - f*spp) % N == r, in order, into a frame
+ * buffer, and one reduce (float sum, to rank 0) per frame over xGMI combines them.  Rank 0 adds each frame
+ * into its context's image (kdpt_read_image, kdpt_save_png) and copies it to `out` when given.  With one
+ * rank, one frame and a zero image, the image equals kdpt_trace_iterations(first, spp, stride 1) bit for bit;
+ * with N ranks it equals the rank partial sums added in the reduce's order.  The calls queue their work and
+ * return (kdpt_synchronize waits); frame f + 1 renders while frame f is reduced.  RCCL (librccl.so.1) is
+ * loaded at run time; KDPT_ERR_UNSUPPORTED when it is absent.
+ * Replaces the reference's single-GPU pathtrace() loop (src/pathtrace.cu:2405-2635, src/main.cpp runCuda). */
+#define KDPT_COMM_ID_BYTES 128
+#define KDPT_REDUCE_RCCL 0  /* ncclReduce (one communicator rank per context) */
+#define KDPT_REDUCE_COPY 1  /* in-process: peer copies to the first device, added in rank order */
+/* One process per GPU: rank 0 makes the id, the caller hands it to every rank (any channel), and each rank
+ * joins with its context (collective: every rank must call it).  id = NULL with nranks > 1: no
+ * communicator; kdpt_render_frames then copies every rank's frame shares to its `out` and the caller reduces
+ * them (e.g. over gloo when ranks share a GPU, which RCCL refuses); the image is left alone. */
+int kdpt_comm_unique_id(unsigned char *id);
+int kdpt_comm_init(kdpt_ctx *ctx, int nranks, int rank, const unsigned char *id);
+/* This rank's share of frames first_frame .. first_frame + frames - 1 (every rank calls it with the same
+ * arguments); out: rank 0, frames * 3*W*H floats, device or host memory, or NULL. */
+int kdpt_render_frames(kdpt_ctx *ctx, int first_frame, int frames, int spp, int pipeline, int batch, float *out);
+/* One process, one context per device (devices[0..ndev), <= 8; a device may repeat with KDPT_REDUCE_COPY):
+ * renders the frames, waits, and frees everything.  out (host or device 0 memory, frames * 3*W*H floats, or
+ * NULL) receives each frame's reduced image. */
+int kdpt_render_sharded(const kdpt_scene *scene, const kdpt_options *opt, int ndev, const int *devices,
+                        int first_frame, int frames, int spp, int pipeline, int batch, int reduce, float *out);
 int kdpt_destroy(kdpt_ctx *ctx);
 const char *kdpt_last_error(void);
 

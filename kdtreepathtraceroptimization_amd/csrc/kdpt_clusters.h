@@ -1,0 +1,275 @@
+// kdpt_clusters.h -- host-side construction of the big-leaf clusters, super-clusters and cluster slabs
+// (DevScene::leaf_cl, cl_lo / cl_hi / cl_n, sup, c_v0 / c_e1 / c_e2).  Shared by the runtime
+// (kdpt_runtime.hip build_clusters, which uploads the result) and the host differential test of the cluster
+// cull (tests/native/cull_diff.cpp), so that the test checks exactly the boxes the kernels read.
+//
+// Only the order in which a wave tests a big leaf's triangles depends on this grouping (results are
+// recombined by original index); the cull is conservative with respect to glm's float u/v tests
+// ("Cluster cull"), which the margin coefficient (cluster_margin) guarantees.
+#pragma once
+
+#include <algorithm>
+#include <cfloat>
+#include <cmath>
+#include <utility>
+#include <vector>
+
+#include "../../include/kdpt.h"
+#include "kdpt_device.h"
+
+namespace kdpt {
+
+// Half-precision bits of the largest half <= x (half_down) / the smallest half >= x (half_up); overflow goes
+// to -inf / +inf, so the rounded value always bounds x (x finite).  Portable (no _Float16): round x to the
+// nearest half through its float bits, then step outward when that rounded up (down).
+inline uint32_t half_nearest(float x) {
+  uint32_t b;
+  memcpy(&b, &x, 4);
+  const uint32_t s = (b >> 16) & 0x8000u;
+  const uint32_t a = b & 0x7fffffffu;
+  if (a >= 0x7f800000u) return s | 0x7c00u | (a > 0x7f800000u ? 0x200u : 0u);  // inf / nan
+  if (a >= 0x477ff000u) return s | 0x7c00u;  // |x| >= 65520: rounds to inf
+  if (a < 0x38800000u) {  // below the smallest normal half (2^-14): subnormal, units of 2^-24
+    const float v = fabsf(x) * 16777216.0f;  // exact (power of two)
+    const float r = nearbyintf(v);           // ties to even under the default rounding mode
+    return s | (uint32_t)r;
+  }
+  const uint32_t e = (a >> 23) - 112u, m = a & 0x7fffffu;
+  uint32_t h = (e << 10) | (m >> 13);
+  const uint32_t rest = m & 0x1fffu;
+  if (rest > 0x1000u || (rest == 0x1000u && (h & 1u))) h++;  // to nearest, ties to even (may carry into e)
+  return s | h;
+}
+inline uint32_t half_down(float x) {
+  uint32_t b = half_nearest(x);
+  if (half_to_float(b) > x) {  // one step towards -inf
+    if (b == 0x0000u) b = 0x8001u;
+    else if (b & 0x8000u) b = b + 1u;
+    else b = b - 1u;
+  }
+  return b;
+}
+inline uint32_t half_up(float x) { return half_down(-x) ^ 0x8000u; }
+
+constexpr double CULL_RHO_CAP = 64.0;  // |e1| |e2| / |e1 x e2| beyond which a triangle counts as a sliver
+
+struct ClusterSet {
+  std::vector<int2> leaf_cl, leaf_sp;  // per node: {first cluster, count} / {first super, count}
+  std::vector<int4> sup;               // super-cluster records (DevScene::sup)
+  std::vector<float4> lo, hi, nrm;     // cluster boxes (w: slab bounds) and slab normals
+  std::vector<float4> cv0, ce1, ce2;   // cluster-order triangles, 64 per cluster (ce1.w = original index)
+  std::vector<int2> info;              // {first entry in cv0, triangle count}
+  bool supers_finite = true;           // every super box is finite in half precision
+};
+
+// Big leaves as clusters of <= 64 triangles: Morton order of the triangle centroids inside the leaf's box,
+// consecutive runs of 64, each with its exact float box, the slab along its summed area vector, and runs of
+// SUPER clusters under one half-precision box rounded outward.
+inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tri_bare* tris,
+                              const std::vector<float4>& tv, const std::vector<float4>& e1,
+                              const std::vector<float4>& e2, ClusterSet& cs) {
+  cs = ClusterSet{};
+  cs.leaf_cl.assign(nn, make_int2(0, 0));
+  cs.leaf_sp.assign(nn, make_int2(0, 0));
+  auto spread = [](uint32_t v) {
+    uint32_t r = 0;
+    for (int b = 0; b < 10; b++) r |= ((v >> b) & 1u) << (3 * b);
+    return r;
+  };
+  for (int i = 0; i < nn; i++) {
+    const kdpt_node_bare& N = nodes[i];
+    if (N.triIdSize < BIG_LEAF) continue;
+    const int start = N.triIdStart, size = N.triIdSize;
+    std::vector<std::pair<uint32_t, int>> key(size);
+    for (int k = 0; k < size; k++) {
+      const kdpt_tri_bare& T = tris[start + k];
+      const double cen[3] = {(T.x1 + (double)T.x2 + T.x3) / 3, (T.y1 + (double)T.y2 + T.y3) / 3,
+                             (T.z1 + (double)T.z2 + T.z3) / 3};
+      uint32_t m = 0;
+      for (int a = 0; a < 3; a++) {
+        const double ext = std::max((double)N.maxs[a] - N.mins[a], 1e-30);
+        const double u = std::min(std::max((cen[a] - N.mins[a]) / ext, 0.0), 1.0);
+        m |= spread((uint32_t)(u * 1023.0)) << a;
+      }
+      key[k] = {m, k};
+    }
+    std::stable_sort(key.begin(), key.end(), [](const std::pair<uint32_t, int>& a,
+                                                const std::pair<uint32_t, int>& b) { return a.first < b.first; });
+    cs.leaf_cl[i] = make_int2((int)cs.info.size(), (size + 63) / 64);
+    for (int b = 0; b < size; b += 64) {
+      const int cnt = std::min(64, size - b);
+      float l[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, h[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
+      cs.info.push_back(make_int2((int)cs.cv0.size(), cnt));
+      for (int k = b; k < b + cnt; k++) {
+        const int t = start + key[k].second;
+        const kdpt_tri_bare& T = tris[t];
+        const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
+        for (int v = 0; v < 3; v++) {
+          l[0] = std::min(l[0], vx[v]); h[0] = std::max(h[0], vx[v]);
+          l[1] = std::min(l[1], vy[v]); h[1] = std::max(h[1], vy[v]);
+          l[2] = std::min(l[2], vz[v]); h[2] = std::max(h[2], vz[v]);
+        }
+        cs.cv0.push_back(tv[t]);
+        float4 q = e1[t];
+        q.w = ibits(t);  // original triangle index
+        cs.ce1.push_back(q);
+        cs.ce2.push_back(e2[t]);
+      }
+      for (int k = cnt; k < 64; k++) {  // padding: e1 = e2 = 0 fails glm's determinant test
+        cs.cv0.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+        cs.ce1.push_back(make_float4(0.0f, 0.0f, 0.0f, ibits(-1)));
+        cs.ce2.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
+      }
+      // the slab: n = the normalised sum of the triangles' (v1 - v0) x (v2 - v0), c as the kernel forms it,
+      // [min, max] of n . (v - c) over the vertices in double, rounded outward to float
+      const float cc[3] = {0.5f * (l[0] + h[0]), 0.5f * (l[1] + h[1]), 0.5f * (l[2] + h[2])};
+      double ns[3] = {0, 0, 0};
+      for (int k = b; k < b + cnt; k++) {
+        const kdpt_tri_bare& T = tris[start + key[k].second];
+        const double ax = (double)T.x2 - T.x1, ay = (double)T.y2 - T.y1, az = (double)T.z2 - T.z1;
+        const double bx = (double)T.x3 - T.x1, by = (double)T.y3 - T.y1, bz = (double)T.z3 - T.z1;
+        ns[0] += ay * bz - az * by;
+        ns[1] += az * bx - ax * bz;
+        ns[2] += ax * by - ay * bx;
+      }
+      const double nl = std::sqrt(ns[0] * ns[0] + ns[1] * ns[1] + ns[2] * ns[2]);
+      float nf[3] = {0.0f, 0.0f, 0.0f};
+      float dlo = -FLT_MAX, dhi = FLT_MAX;
+      if (nl > 0 && std::isfinite(nl)) {
+        for (int a = 0; a < 3; a++) nf[a] = (float)(ns[a] / nl);
+        double mn = 1e300, mx = -1e300;
+        for (int k = b; k < b + cnt; k++) {
+          const kdpt_tri_bare& T = tris[start + key[k].second];
+          const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
+          for (int v = 0; v < 3; v++) {
+            const double dv = (double)nf[0] * ((double)vx[v] - cc[0]) + (double)nf[1] * ((double)vy[v] - cc[1]) +
+                              (double)nf[2] * ((double)vz[v] - cc[2]);
+            mn = std::min(mn, dv);
+            mx = std::max(mx, dv);
+          }
+        }
+        dlo = std::nextafter((float)mn, -FLT_MAX);
+        dhi = std::nextafter((float)mx, FLT_MAX);
+      }
+      // the spread of the triangles' normals about nf (slab level's direction-dependent margin,
+      // cull_margin_dir): the largest chord |N_t / |N_t| - nf| over the cluster, N_t = e1 x e2 of glm's float
+      // edges, rounded up; 4 (never a usable lower bound) when nf = 0 or a triangle is a sliver
+      // (|e1| |e2| / |N_t| > CULL_RHO_CAP) that could still pass glm's determinant test
+      double spread = (nl > 0 && std::isfinite(nl)) ? 0.0 : 4.0;
+      for (int k = b; k < b + cnt && spread < 4.0; k++) {
+        const int e = cs.info.back().x + (k - b);
+        const double ax = cs.ce1[e].x, ay = cs.ce1[e].y, az = cs.ce1[e].z;
+        const double bx = cs.ce2[e].x, by = cs.ce2[e].y, bz = cs.ce2[e].z;
+        const double Nx = ay * bz - az * by, Ny = az * bx - ax * bz, Nz = ax * by - ay * bx;
+        const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+        const double E = std::sqrt(ax * ax + ay * ay + az * az) * std::sqrt(bx * bx + by * by + bz * bz);
+        if (Nl == 0.0 || E > CULL_RHO_CAP * Nl) {
+          if (E > 0.3) spread = 4.0;  // (|a| <= 5.8 u E < FLT_EPSILON otherwise: it never passes)
+          continue;
+        }
+        const double cx = Nx / Nl - nf[0], cy = Ny / Nl - nf[1], cz = Nz / Nl - nf[2];
+        spread = std::max(spread, std::sqrt(cx * cx + cy * cy + cz * cz));
+      }
+      const float sf = std::nextafter((float)std::min(spread, 4.0), FLT_MAX);
+      cs.lo.push_back(make_float4(l[0], l[1], l[2], dlo));
+      cs.hi.push_back(make_float4(h[0], h[1], h[2], dhi));
+      cs.nrm.push_back(make_float4(nf[0], nf[1], nf[2], sf));
+    }
+    const int c0 = cs.leaf_cl[i].x, ncl = cs.leaf_cl[i].y;
+    cs.leaf_sp[i] = make_int2((int)cs.sup.size(), (ncl + SUPER - 1) / SUPER);
+    for (int b = 0; b < ncl; b += SUPER) {
+      const int cnt = std::min(SUPER, ncl - b);
+      float4 sl = cs.lo[c0 + b], sh = cs.hi[c0 + b];
+      for (int k = c0 + b + 1; k < c0 + b + cnt; k++) {
+        sl.x = std::min(sl.x, cs.lo[k].x); sl.y = std::min(sl.y, cs.lo[k].y); sl.z = std::min(sl.z, cs.lo[k].z);
+        sh.x = std::max(sh.x, cs.hi[k].x); sh.y = std::max(sh.y, cs.hi[k].y); sh.z = std::max(sh.z, cs.hi[k].z);
+      }
+      // half precision rounded outward: the stored box holds the exact one
+      const uint32_t lx = half_down(sl.x), ly = half_down(sl.y), lz = half_down(sl.z);
+      const uint32_t hx = half_up(sh.x), hy = half_up(sh.y), hz = half_up(sh.z);
+      for (uint32_t q : {lx, ly, lz, hx, hy, hz})
+        if ((q & 0x7c00u) == 0x7c00u) cs.supers_finite = false;  // beyond the half range: no super route
+      cs.sup.push_back(make_int4((int)(lx | ly << 16), (int)(lz | hx << 16), (int)(hy | hz << 16),
+                                 (int)((uint32_t)(c0 + b) << 5 | (uint32_t)(cnt - 1))));
+    }
+  }
+}
+
+// The brute-force route's boxes of 64 file-order triangles [64j, 64j + 64): the triangles glm tests,
+// v0, v0 + e1, v0 + e2, exact in double and rounded outward to float (BruteArgs::chunk_lo / chunk_hi).
+inline void build_chunk_boxes(const std::vector<float4>& tv, const std::vector<float4>& e1,
+                              const std::vector<float4>& e2, int nt, std::vector<float4>& clo,
+                              std::vector<float4>& chi) {
+  const int nch = std::max(1, (nt + 63) / 64);
+  clo.assign(nch, make_float4(0, 0, 0, 0));
+  chi.assign(nch, make_float4(0, 0, 0, 0));
+  for (int j = 0; j < nch; j++) {
+    double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
+    for (int k = 64 * j; k < std::min(nt, 64 * j + 64); k++) {
+      const double v[3] = {tv[k].x, tv[k].y, tv[k].z}, a[3] = {e1[k].x, e1[k].y, e1[k].z},
+                   b[3] = {e2[k].x, e2[k].y, e2[k].z};
+      for (int r = 0; r < 3; r++) {  // the triangle glm tests: v0 + u e1 + v e2, exact in double
+        lo[r] = std::min({lo[r], v[r], v[r] + a[r], v[r] + b[r]});
+        hi[r] = std::max({hi[r], v[r], v[r] + a[r], v[r] + b[r]});
+      }
+    }
+    float l[3], h[3];
+    for (int r = 0; r < 3; r++) {
+      if (lo[r] > hi[r]) lo[r] = hi[r] = 0.0;  // empty chunk (no triangles)
+      l[r] = (float)lo[r];
+      if ((double)l[r] > lo[r]) l[r] = std::nextafter(l[r], -FLT_MAX);
+      h[r] = (float)hi[r];
+      if ((double)h[r] < hi[r]) h[r] = std::nextafter(h[r], FLT_MAX);
+    }
+    clo[j] = make_float4(l[0], l[1], l[2], 0.0f);
+    chi[j] = make_float4(h[0], h[1], h[2], 0.0f);
+  }
+}
+
+// The cluster cull's margin coefficient K (DevScene::cl_margin; cluster_may_pass widens a box by
+// K (1 + |o - c|_1 + size_1)).  A triangle can pass glm's float u/v tests for a line that misses it: the
+// computed (u, v) carry rounding errors of order u |o - v0| |e1| |e2| / a (a: glm's determinant), and a may
+// be as small as FLT_EPSILON.  DESIGN.md 4 ("Cluster cull") bounds the distance from the line to the point
+// v0 + u e1 + v e2 the float test accepts by 17.34 u |o - v0| |e1| |e2| / a + 2.1 u max|e|; with a >= FLT_EPSILON
+// = 2u that is 8.67 |o - v0| E + ..., E = |e1| |e2|.  So K_rigorous = 8.75 E_max + 64 u (1 + max|coord| +
+// max|e|) makes the cull conservative for EVERY line (the constant term covers the box and slab tests' own
+// rounding).  Meshes of small triangles (the C5 icosphere: E_max = 1.07e-4, K = 9.4e-4) get it; for meshes of
+// large triangles it would cull nothing (dragon_5: E_max = 0.2), so they keep K = 1e-4, conservative except
+// for lines lying within ~17 u |o - v0| of a triangle's plane and within ~17 u rho / K of parallel to it
+// (tests/native/cull_diff.cpp constructs such lines); the "cluster_cull" knob = 0 removes the cull.
+struct CullMargin {
+  float K;          // the box-only tests' coefficient (DevScene::cl_margin)
+  float K_lo;       // the slab level's floor (cl_margin_lo)
+  float a, b, c;    // the slab level's direction-dependent bound (cull_a, cull_b, cull_c)
+  double rigorous;  // K_rigorous for these triangles
+  bool exact;       // K >= K_rigorous: the cull never drops a triangle that passes glm's u/v tests
+};
+constexpr float CULL_MARGIN_FAST = 1e-4f;  // the margin of meshes whose K_rigorous exceeds the cap
+constexpr double CULL_MARGIN_CAP = 2e-3;   // largest K_rigorous worth using (beyond it the cull loses its bite)
+inline CullMargin cluster_margin(const std::vector<float4>& v0, const std::vector<float4>& e1,
+                                 const std::vector<float4>& e2) {
+  double emax = 0.0, pmax = 0.0, cmax = 0.0, rho = 1.0;
+  for (size_t i = 0; i < e1.size(); i++) {
+    const double ax = e1[i].x, ay = e1[i].y, az = e1[i].z, bx = e2[i].x, by = e2[i].y, bz = e2[i].z;
+    const double a = std::sqrt(ax * ax + ay * ay + az * az), b = std::sqrt(bx * bx + by * by + bz * bz);
+    const double Nx = ay * bz - az * by, Ny = az * bx - ax * bz, Nz = ax * by - ay * bx;
+    const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+    emax = std::max(emax, std::max(a, b));
+    pmax = std::max(pmax, a * b);
+    if (Nl > 0.0 && a * b <= CULL_RHO_CAP * Nl) rho = std::max(rho, a * b / Nl);  // slivers: spread 4
+    cmax = std::max(cmax, std::max(std::fabs((double)v0[i].x), std::max(std::fabs((double)v0[i].y),
+                                                                           std::fabs((double)v0[i].z))) + a + b);
+  }
+  const double u = 5.9604644775390625e-8;  // 2^-24
+  CullMargin r;
+  r.rigorous = 8.75 * pmax + 64.0 * u * (1.0 + cmax + emax);
+  r.exact = r.rigorous <= CULL_MARGIN_CAP;
+  r.K_lo = CULL_MARGIN_FAST;
+  r.K = r.exact ? std::max(std::nextafter((float)r.rigorous, FLT_MAX), CULL_MARGIN_FAST) : CULL_MARGIN_FAST;
+  r.a = std::nextafter((float)(17.5 * u * rho * (1.0 + 1e-5)), FLT_MAX);
+  r.b = std::nextafter((float)(5.8 * u * rho + 10.0 * u), FLT_MAX);
+  r.c = std::nextafter((float)(64.0 * u * (1.0 + cmax + emax)), FLT_MAX);
+  return r;
+}
+
+}  // namespace kdpt

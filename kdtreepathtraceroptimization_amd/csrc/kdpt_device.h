@@ -125,6 +125,10 @@ struct DevScene {
   // The two-level cull tests the line against this slab as well as the box (knob "cluster_slab")
   const float4* cl_n;
   int cl_slab;
+  // the cull's margin coefficients (kdpt_clusters.h cluster_margin): cl_margin for the box-only tests;
+  // the slab level uses cull_margin_dir(): max(cl_margin_lo, min(cl_margin, cull_a / g + cull_c)),
+  // g = |n . d| - cl_n.w - cull_b
+  float cl_margin, cl_margin_lo, cull_a, cull_b, cull_c;
   const int4* snodes;
   const float4* c_v0;
   const float4* c_e1;
@@ -405,6 +409,97 @@ KDPT_HD int tri_test_v(const TriData& T, f3 o, f3 d, float& bx, float& by, float
   return (bz >= 0.0f) ? 2 : 1;
 }
 
+// ---------------------------------------------------------------------------
+// Big leaves (>= BIG_LEAF triangles) are swept in clusters of 64; the C5 route groups SUPER clusters under
+// one half-precision box.  The cluster cull below is host-compilable so that tests/native/cull_diff.cpp
+// can check it against tri_test_v on adversarial lines ("Cluster cull").
+// ---------------------------------------------------------------------------
+#ifndef KDPT_SUPER
+#define KDPT_SUPER 16  // tools/build_variant.sh experiments only (a power of two <= 64)
+#endif
+constexpr int SUPER = KDPT_SUPER;  // clusters per super-cluster
+#ifndef KDPT_BIG_LEAF
+#define KDPT_BIG_LEAF 64  // tools/build_variant.sh experiments only
+#endif
+constexpr int BIG_LEAF = KDPT_BIG_LEAF;  // leaves this size or larger are tested cluster by cluster
+
+// IEEE half bits -> float (exact).  The device converts in one instruction; g++ 11 has no _Float16.
+KDPT_HD float half_to_float(uint32_t h) {
+#if defined(__clang__)
+  return (float)__builtin_bit_cast(_Float16, (unsigned short)(h & 0xffffu));
+#else
+  const uint32_t s = (h & 0x8000u) << 16, e = (h >> 10) & 0x1fu, m = h & 0x3ffu;
+  uint32_t b;
+  if (e == 0x1fu) b = s | 0x7f800000u | (m << 13);
+  else if (e) b = s | ((e + 112u) << 23) | (m << 13);
+  else if (!m) b = s;
+  else {  // subnormal half: m x 2^-24, exact in float
+    const float v = (float)m * 5.9604644775390625e-8f;
+    return s ? -v : v;
+  }
+  float f;
+  memcpy(&f, &b, 4);
+  return f;
+#endif
+}
+KDPT_HD float half_lo(uint32_t w) { return half_to_float(w & 0xffffu); }
+KDPT_HD float half_hi(uint32_t w) { return half_to_float(w >> 16); }
+
+// May the LINE through o (both directions: glm's u/v tests ignore the sign of t) cross the cluster's
+// triangles?  The box is widened by 1e-4 x (distance + size), orders of magnitude above the rounding
+// of the Moller-Trumbore u/v tests, so a culled cluster holds no triangle that would pass them.
+KDPT_HD bool cluster_may_pass(float4 lo, float4 hi, f3 o, f3 inv, float K) {
+  const float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
+  const float m = K * (1.0f + fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) + (hi.x - lo.x) +
+                           (hi.y - lo.y) + (hi.z - lo.z));
+  const float t1x = (lo.x - m - o.x) * inv.x, t2x = (hi.x + m - o.x) * inv.x;
+  const float t1y = (lo.y - m - o.y) * inv.y, t2y = (hi.y + m - o.y) * inv.y;
+  const float t1z = (lo.z - m - o.z) * inv.z, t2z = (hi.z + m - o.z) * inv.z;
+  const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
+  const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+  return tmin <= tmax;
+}
+
+// The margin coefficient of the slab level for a line of direction d and a cluster of normal n (n.w = the
+// largest chord |N_t / |N_t| - n| over the cluster's triangles): glm's determinant of every triangle t of the
+// cluster is then at least |N_t| (|n . d| - n.w - cull_b), which bounds the float u/v error and so the margin a
+// u/v pass can need ("Cluster cull"); min with the direction-free rigorous cl_margin, max with
+// the fast floor cl_margin_lo.  A line nearly parallel to the cluster's patch gets the direction-free one.
+struct CullK {
+  float hi, lo, a, b, c;  // DevScene::cl_margin, cl_margin_lo, cull_a, cull_b, cull_c
+};
+KDPT_HD float cull_margin_dir(float nd, float spread, const CullK& k) {
+  const float g = fabsf(nd) - spread - k.b;
+  const float kd = g > 0.0f ? k.a / g + k.c : k.hi;
+  return fmaxf(k.lo, fminf(k.hi, kd));
+}
+
+// cluster_may_pass and the cluster's slab {q : n . (q - c) in [lo.w, hi.w]}: the line's parameter interval
+// through the slab, widened by the same margin, must meet its interval through the box.  A triangle the line
+// crosses has its crossing point in both (a convex combination of its vertices), so the cull stays
+// conservative; a line (nearly) parallel to the slab passes it.  A curved-surface patch is thin along its
+// normal, so a line that only grazes the patch's box is culled.
+KDPT_HD bool cluster_may_pass_slab(float4 lo, float4 hi, float4 n, f3 o, f3 inv, f3 d, const CullK& k) {
+  const float nd = n.x * d.x + n.y * d.y + n.z * d.z;
+  const float K = cull_margin_dir(nd, n.w, k);
+  const float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
+  const float m = K * (1.0f + fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) + (hi.x - lo.x) +
+                           (hi.y - lo.y) + (hi.z - lo.z));
+  const float t1x = (lo.x - m - o.x) * inv.x, t2x = (hi.x + m - o.x) * inv.x;
+  const float t1y = (lo.y - m - o.y) * inv.y, t2y = (hi.y + m - o.y) * inv.y;
+  const float t1z = (lo.z - m - o.z) * inv.z, t2z = (hi.z + m - o.z) * inv.z;
+  float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
+  float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+  const float no = n.x * (o.x - cx) + n.y * (o.y - cy) + n.z * (o.z - cz);
+  if (fabsf(nd) > 1e-12f) {
+    const float rn = 1.0f / nd;
+    const float s1 = (lo.w - m - no) * rn, s2 = (hi.w + m - no) * rn;
+    tmin = fmaxf(tmin, fminf(s1, s2));
+    tmax = fminf(tmax, fmaxf(s1, s2));
+  }
+  return tmin <= tmax;
+}
+
 #if defined(__HIPCC__) || defined(__HIP__)
 // ---------------------------------------------------------------------------
 // Wave-cooperative form of traverseKD for gfx950 (64-lane waves).
@@ -580,8 +675,6 @@ struct ClustersInterleaved {
 };
 // Two-level: the super-cluster records in LDS (16 bytes: half-precision box rounded outward, first cluster
 // and count), the cluster boxes in HBM/L2.
-__device__ inline float half_lo(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w & 0xffffu)); }
-__device__ inline float half_hi(uint32_t w) { return (float)__builtin_bit_cast(_Float16, (unsigned short)(w >> 16)); }
 struct ClustersSuper {
   static constexpr bool kSuper = true;
   const int4* sp;
@@ -601,10 +694,6 @@ struct ClustersSuper {
   __device__ float4 lo_of(int c) const { return lo[c]; }
   __device__ float4 hi_of(int c) const { return hi[c]; }
 };
-#ifndef KDPT_SUPER
-#define KDPT_SUPER 16  // tools/build_variant.sh experiments only (a power of two <= 64)
-#endif
-constexpr int SUPER = KDPT_SUPER;  // clusters per super-cluster
 
 struct WaveLeafLDS {
   int slot[64];    // pair_owner's scatter slots (all zero between calls)
@@ -637,10 +726,6 @@ __device__ inline void prof_lap(WaveProf* P, int k) {  // cycles since the last 
   }
 }
 
-#ifndef KDPT_BIG_LEAF
-#define KDPT_BIG_LEAF 64  // tools/build_variant.sh experiments only
-#endif
-constexpr int BIG_LEAF = KDPT_BIG_LEAF;  // leaves this size or larger are tested cluster by cluster
 
 // number of set bits of mask below this lane
 __device__ inline unsigned int lane_prefix(unsigned long long mask) {
@@ -709,46 +794,6 @@ __device__ inline int wave_max_i32(int v) {
   KDPT_WAVE_REDUCE(KDPT_STEP)
 #undef KDPT_STEP
   return __builtin_amdgcn_readlane(v, 63);
-}
-
-// May the LINE through o (both directions: glm's u/v tests ignore the sign of t) cross the cluster's
-// triangles?  The box is widened by 1e-4 x (distance + size), orders of magnitude above the rounding
-// of the Moller-Trumbore u/v tests, so a culled cluster holds no triangle that would pass them.
-__device__ inline bool cluster_may_pass(float4 lo, float4 hi, f3 o, f3 inv) {
-  const float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
-  const float m = 1e-4f * (1.0f + fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) + (hi.x - lo.x) +
-                           (hi.y - lo.y) + (hi.z - lo.z));
-  const float t1x = (lo.x - m - o.x) * inv.x, t2x = (hi.x + m - o.x) * inv.x;
-  const float t1y = (lo.y - m - o.y) * inv.y, t2y = (hi.y + m - o.y) * inv.y;
-  const float t1z = (lo.z - m - o.z) * inv.z, t2z = (hi.z + m - o.z) * inv.z;
-  const float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
-  const float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
-  return tmin <= tmax;
-}
-
-// cluster_may_pass and the cluster's slab {q : n . (q - c) in [lo.w, hi.w]}: the line's parameter interval
-// through the slab, widened by the same margin, must meet its interval through the box.  A triangle the line
-// crosses has its crossing point in both (a convex combination of its vertices), so the cull stays
-// conservative; a line (nearly) parallel to the slab passes it.  A curved-surface patch is thin along its
-// normal, so a line that only grazes the patch's box is culled.
-__device__ inline bool cluster_may_pass_slab(float4 lo, float4 hi, float4 n, f3 o, f3 inv, f3 d) {
-  const float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
-  const float m = 1e-4f * (1.0f + fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) + (hi.x - lo.x) +
-                           (hi.y - lo.y) + (hi.z - lo.z));
-  const float t1x = (lo.x - m - o.x) * inv.x, t2x = (hi.x + m - o.x) * inv.x;
-  const float t1y = (lo.y - m - o.y) * inv.y, t2y = (hi.y + m - o.y) * inv.y;
-  const float t1z = (lo.z - m - o.z) * inv.z, t2z = (hi.z + m - o.z) * inv.z;
-  float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
-  float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
-  const float nd = n.x * d.x + n.y * d.y + n.z * d.z;
-  const float no = n.x * (o.x - cx) + n.y * (o.y - cy) + n.z * (o.z - cz);
-  if (fabsf(nd) > 1e-12f) {
-    const float rn = 1.0f / nd;
-    const float s1 = (lo.w - m - no) * rn, s2 = (hi.w + m - no) * rn;
-    tmin = fmaxf(tmin, fminf(s1, s2));
-    tmax = fminf(tmax, fmaxf(s1, s2));
-  }
-  return tmin <= tmax;
 }
 
 __device__ inline void wave_lds_sync() {
@@ -1115,7 +1160,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         if (fastAABB) {
           const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
-          if (pass) pass = cluster_may_pass(slo, shi, oo, ii);
+          if (pass) pass = cluster_may_pass(slo, shi, oo, ii, S.cl_margin);
         }
         const unsigned long long sm = __ballot(pass);
         const int nsv = __popcll(sm);
@@ -1138,10 +1183,11 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
             const f3 ii =
                 mk3(bpermute_f(invdir.x, cown), bpermute_f(invdir.y, cown), bpermute_f(invdir.z, cown));
             if (S.cl_slab) {
+              const CullK ck{S.cl_margin, S.cl_margin_lo, S.cull_a, S.cull_b, S.cull_c};
               const f3 dd = mk3(bpermute_f(d.x, cown), bpermute_f(d.y, cown), bpermute_f(d.z, cown));
-              if (cp) cp = cluster_may_pass_slab(clusters.lo_of(c), clusters.hi_of(c), clusters.n_of(c), oo, ii, dd);
+              if (cp) cp = cluster_may_pass_slab(clusters.lo_of(c), clusters.hi_of(c), clusters.n_of(c), oo, ii, dd, ck);
             } else {
-              if (cp) cp = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
+              if (cp) cp = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii, S.cl_margin);
             }
           }
           if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
@@ -1171,7 +1217,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         if (fastAABB) {
           const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
-          if (pass) pass = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
+          if (pass) pass = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii, S.cl_margin);
         }
         if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
         sweep(pass, c, own);

@@ -21,11 +21,16 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <vector>
 
+#include <dlfcn.h>
+#include <rccl/rccl.h>
+
 #include "../../include/kdpt.h"
 #include "kdpt_device.h"
+#include "kdpt_clusters.h"
 
 using namespace kdpt;
 
@@ -196,7 +201,7 @@ constexpr int trace_block() { return MODE == 2 ? TRACE_BLOCK : (MODE >= 3 ? TRAC
 // Up to MAXB iterations (each its own path buffers) at the same bounce share one intersect launch:
 // more rays per launch keep the lanes of the persistent waves busy.
 #ifndef KDPT_MAXB
-#define KDPT_MAXB 8  // tools/build_variant.sh experiments only
+#define KDPT_MAXB 16  // tools/build_variant.sh experiments only
 #endif
 constexpr int MAXB = KDPT_MAXB;
 struct TraceIter {
@@ -832,7 +837,7 @@ __global__ __launch_bounds__(TILE) void k_brute(BruteArgs A) {
           // can hit; the others test its triangles in file order as before
           for (int k = k0; k < k0 + nt;) {
             const int j = k >> 6, kend = min(k0 + nt, (j + 1) << 6);
-            const bool may = take && (!cull || cluster_may_pass(A.chunk_lo[j], A.chunk_hi[j], o, inv));
+            const bool may = take && (!cull || cluster_may_pass(A.chunk_lo[j], A.chunk_hi[j], o, inv, S.cl_margin));
             if (__any(may)) {
               for (; k < kend; k++) {
                 const TriData T = tri_load(S, k);
@@ -1680,6 +1685,7 @@ struct kdpt_ctx {
   bool grid_env = false;  // trace_grid fixed by the "trace_grid_frac" tuning knob
   bool force_global_tree = false;  // "tree_global" tuning knob: keep the tree in HBM/L2
   bool super_cull = true;          // "super_cull" tuning knob: 0 = no TREE_LDS16S route (one-level cull)
+  CullMargin cull{};                // the scene's cluster-cull margins (kdpt_clusters.h cluster_margin)
   int tree_format = 0;             // "tree_format" knob: 16 / 32 = LDS node records of that size only
   size_t tree_lds = 0;    // dynamic LDS bytes of the intersect kernel (TREE_LDS)
   int* tile_counts = nullptr;
@@ -1732,6 +1738,16 @@ struct kdpt_ctx {
   int num_shapes = 0;
   float4* chunk_lo = nullptr;  // brute force: boxes of 64 file-order triangles
   float4* chunk_hi = nullptr;
+  // spp-sharded frames (kdpt_comm_init / kdpt_render_frames / kdpt_render_sharded): this context's rank, the
+  // RCCL communicator (null: one rank, or the in-process copy reduce of kdpt_render_sharded), two frame
+  // buffers (frame f accumulates into frame_buf[f & 1] while f - 1 is reduced) and rank 0's reduced frame
+  int nranks = 1, rank = 0;
+  void* comm = nullptr;  // ncclComm_t
+  bool owns_comm = false;
+  bool external_reduce = false;  // kdpt_comm_init without an id: each rank hands its frame shares out
+  float* frame_buf[2] = {nullptr, nullptr};
+  float* frame_sum = nullptr;
+  hipEvent_t frame_ev[2] = {nullptr, nullptr};  // frame_buf[k] consumed by its reduce (copy-reduce mode)
 };
 
 namespace {
@@ -1754,6 +1770,7 @@ int dupload(kdpt_ctx* c, T** p, const T* src, size_t n) {
 }
 
 int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count);
+void release_comm(kdpt_ctx* c);  // (multi-GPU section, end of file)
 int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, int stop_depth, bool count,
                  std::vector<hipEvent_t>* bev);
 
@@ -1921,131 +1938,30 @@ int drain_intersect_events(kdpt_ctx* c) {
   return KDPT_OK;
 }
 
-// Half-precision bits of the largest half <= x (half_down) / the smallest half >= x (half_up); overflow goes
-// to -inf / +inf, so the rounded value always bounds x (x finite).
-uint32_t half_down(float x) {
-  const _Float16 h0 = (_Float16)x;  // round to nearest
-  uint16_t b = __builtin_bit_cast(uint16_t, h0);
-  if ((float)h0 > x) {  // one step towards -inf
-    if (b == 0x0000u) b = 0x8001u;
-    else if (b & 0x8000u) b = (uint16_t)(b + 1u);
-    else b = (uint16_t)(b - 1u);
-  }
-  return b;
+// The scene's cull margins (kdpt_clusters.h cluster_margin) into the context and its DevScene; fixed: one
+// direction-free coefficient for every level (tuning "cull_margin" / "cluster_cull" = 0, which passes inf).
+void set_cull(kdpt_ctx* c, const CullMargin& cm) {
+  c->cull = cm;
+  c->S.cl_margin = cm.K;
+  c->S.cl_margin_lo = cm.K_lo;
+  c->S.cull_a = cm.a;
+  c->S.cull_b = cm.b;
+  c->S.cull_c = cm.c;
 }
-uint32_t half_up(float x) { return half_down(-x) ^ 0x8000u; }
+void fix_cull(kdpt_ctx* c, float K) {
+  c->S.cl_margin = c->S.cl_margin_lo = K;
+}
 
-// Big leaves as clusters of <= 64 triangles (kdpt_device.h DevScene::leaf_cl ...): Morton order of
-// the triangle centroids inside the leaf's box, consecutive runs of 64, each with its exact float box.
-// Only the order in which the wave tests a big leaf's triangles changes; results are recombined by
-// original index, so any grouping is exact.
+// Big leaves as clusters of <= 64 triangles, super-clusters and slabs (kdpt_clusters.h), uploaded.
 int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>& tv, const std::vector<float4>& e1,
                    const std::vector<float4>& e2, std::vector<int2>& leaf_cl, std::vector<int2>& leaf_sp) {
-  const int nn = sc->num_nodes;
-  leaf_cl.assign(nn, make_int2(0, 0));
-  leaf_sp.assign(nn, make_int2(0, 0));
-  std::vector<int4> sp;  // super-clusters: SUPER consecutive clusters of one leaf (DevScene::sup)
-  std::vector<float4> lo, hi, nrm, cv0, ce1, ce2;
-  std::vector<int2> info;
-  auto spread = [](uint32_t v) {
-    uint32_t r = 0;
-    for (int b = 0; b < 10; b++) r |= ((v >> b) & 1u) << (3 * b);
-    return r;
-  };
-  for (int i = 0; i < nn; i++) {
-    const kdpt_node_bare& N = sc->nodes[i];
-    if (N.triIdSize < BIG_LEAF) continue;
-    const int start = N.triIdStart, size = N.triIdSize;
-    std::vector<std::pair<uint32_t, int>> key(size);
-    for (int k = 0; k < size; k++) {
-      const kdpt_tri_bare& T = sc->tris[start + k];
-      const double cen[3] = {(T.x1 + (double)T.x2 + T.x3) / 3, (T.y1 + (double)T.y2 + T.y3) / 3,
-                             (T.z1 + (double)T.z2 + T.z3) / 3};
-      uint32_t m = 0;
-      for (int a = 0; a < 3; a++) {
-        const double ext = std::max((double)N.maxs[a] - N.mins[a], 1e-30);
-        const double u = std::min(std::max((cen[a] - N.mins[a]) / ext, 0.0), 1.0);
-        m |= spread((uint32_t)(u * 1023.0)) << a;
-      }
-      key[k] = {m, k};
-    }
-    std::stable_sort(key.begin(), key.end(), [](const auto& a, const auto& b) { return a.first < b.first; });
-    leaf_cl[i] = make_int2((int)info.size(), (size + 63) / 64);
-    for (int b = 0; b < size; b += 64) {
-      const int cnt = std::min(64, size - b);
-      float l[3] = {FLT_MAXV, FLT_MAXV, FLT_MAXV}, h[3] = {-FLT_MAXV, -FLT_MAXV, -FLT_MAXV};
-      info.push_back(make_int2((int)cv0.size(), cnt));
-      for (int k = b; k < b + cnt; k++) {
-        const int t = start + key[k].second;
-        const kdpt_tri_bare& T = sc->tris[t];
-        const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
-        for (int v = 0; v < 3; v++) {
-          l[0] = std::min(l[0], vx[v]); h[0] = std::max(h[0], vx[v]);
-          l[1] = std::min(l[1], vy[v]); h[1] = std::max(h[1], vy[v]);
-          l[2] = std::min(l[2], vz[v]); h[2] = std::max(h[2], vz[v]);
-        }
-        cv0.push_back(tv[t]);
-        float4 q = e1[t];
-        q.w = ibits(t);  // original triangle index
-        ce1.push_back(q);
-        ce2.push_back(e2[t]);
-      }
-      for (int k = cnt; k < 64; k++) {  // padding: e1 = e2 = 0 fails glm's determinant test
-        cv0.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-        ce1.push_back(make_float4(0.0f, 0.0f, 0.0f, ibits(-1)));
-        ce2.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
-      }
-      // the slab: n = the normalised sum of the triangles' (v1 - v0) x (v2 - v0), c as the kernel forms it,
-      // [min, max] of n . (v - c) over the vertices in double, rounded outward to float
-      const float cc[3] = {0.5f * (l[0] + h[0]), 0.5f * (l[1] + h[1]), 0.5f * (l[2] + h[2])};
-      double ns[3] = {0, 0, 0};
-      for (int k = b; k < b + cnt; k++) {
-        const kdpt_tri_bare& T = sc->tris[start + key[k].second];
-        const double ax = (double)T.x2 - T.x1, ay = (double)T.y2 - T.y1, az = (double)T.z2 - T.z1;
-        const double bx = (double)T.x3 - T.x1, by = (double)T.y3 - T.y1, bz = (double)T.z3 - T.z1;
-        ns[0] += ay * bz - az * by;
-        ns[1] += az * bx - ax * bz;
-        ns[2] += ax * by - ay * bx;
-      }
-      const double nl = std::sqrt(ns[0] * ns[0] + ns[1] * ns[1] + ns[2] * ns[2]);
-      float nf[3] = {0.0f, 0.0f, 0.0f};
-      float dlo = -FLT_MAXV, dhi = FLT_MAXV;
-      if (nl > 0 && std::isfinite(nl)) {
-        for (int a = 0; a < 3; a++) nf[a] = (float)(ns[a] / nl);
-        double mn = 1e300, mx = -1e300;
-        for (int k = b; k < b + cnt; k++) {
-          const kdpt_tri_bare& T = sc->tris[start + key[k].second];
-          const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
-          for (int v = 0; v < 3; v++) {
-            const double dv = (double)nf[0] * ((double)vx[v] - cc[0]) + (double)nf[1] * ((double)vy[v] - cc[1]) +
-                              (double)nf[2] * ((double)vz[v] - cc[2]);
-            mn = std::min(mn, dv);
-            mx = std::max(mx, dv);
-          }
-        }
-        dlo = std::nextafter((float)mn, -FLT_MAXV);
-        dhi = std::nextafter((float)mx, FLT_MAXV);
-      }
-      lo.push_back(make_float4(l[0], l[1], l[2], dlo));
-      hi.push_back(make_float4(h[0], h[1], h[2], dhi));
-      nrm.push_back(make_float4(nf[0], nf[1], nf[2], 0.0f));
-    }
-    const int c0 = leaf_cl[i].x, ncl = leaf_cl[i].y;
-    leaf_sp[i] = make_int2((int)sp.size(), (ncl + SUPER - 1) / SUPER);
-    for (int b = 0; b < ncl; b += SUPER) {
-      const int cnt = std::min(SUPER, ncl - b);
-      float4 sl = lo[c0 + b], sh = hi[c0 + b];
-      for (int k = c0 + b + 1; k < c0 + b + cnt; k++) {
-        sl.x = std::min(sl.x, lo[k].x); sl.y = std::min(sl.y, lo[k].y); sl.z = std::min(sl.z, lo[k].z);
-        sh.x = std::max(sh.x, hi[k].x); sh.y = std::max(sh.y, hi[k].y); sh.z = std::max(sh.z, hi[k].z);
-      }
-      // half precision rounded outward: the stored box holds the exact one
-      const uint32_t lx = half_down(sl.x), ly = half_down(sl.y), lz = half_down(sl.z);
-      const uint32_t hx = half_up(sh.x), hy = half_up(sh.y), hz = half_up(sh.z);
-      sp.push_back(make_int4((int)(lx | ly << 16), (int)(lz | hx << 16), (int)(hy | hz << 16),
-                             (int)((uint32_t)(c0 + b) << 5 | (uint32_t)(cnt - 1))));
-    }
-  }
+  ClusterSet cs;
+  build_cluster_set(sc->nodes, sc->num_nodes, sc->tris, tv, e1, e2, cs);
+  leaf_cl = cs.leaf_cl;
+  leaf_sp = cs.leaf_sp;
+  const std::vector<int4>& sp = cs.sup;
+  const std::vector<float4>&lo = cs.lo, &hi = cs.hi, &nrm = cs.nrm, &cv0 = cs.cv0, &ce1 = cs.ce1, &ce2 = cs.ce2;
+  const std::vector<int2>& info = cs.info;
   int2 *dl, *di;
   float4 *dlo, *dhi, *dv0, *de1, *de2;
   int rc;
@@ -2059,8 +1975,11 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
   if ((rc = dupload(c, &dsp, sp.data(), sp.size())) || (rc = dupload(c, &dn, nrm.data(), nrm.size()))) return rc;
   c->S.cl_n = dn;
   c->S.cl_slab = 1;
+  set_cull(c, cluster_margin(cv0, ce1, ce2));
   c->S.sup = dsp;
-  c->S.num_supers = (int)sp.size();
+  // a super box past the half range (+-65504) would be infinite, its centre NaN and the cull wrong: such a
+  // scene gets no super-cluster route (TREE_LDS16S needs num_supers > 0)
+  c->S.num_supers = cs.supers_finite ? (int)sp.size() : 0;
   c->S.leaf_cl = dl;
   c->S.num_clusters = (int)info.size();
   c->S.cl_info = di;
@@ -2441,6 +2360,7 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   c->S.num_nodes = sc->has_obj ? sc->num_nodes : 0;
   c->S.root = 0;
   c->S.n0_left = c->S.n0_right = c->S.n1_left = c->S.n1_right = -1;
+  set_cull(c, cluster_margin({}, {}, {}));  // (no triangles: the fast margin; replaced below)
   if (sc->has_obj && sc->num_nodes > 0 && !brute) {
     const int nn = sc->num_nodes, nt = sc->num_tris;
     std::vector<int4> nodes(4 * (size_t)nn);
@@ -2528,29 +2448,9 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
       n1[k] = make_float4(nb[0], nb[1], nb[2], 0.0f);
       n2[k] = make_float4(nc[0], nc[1], nc[2], 0.0f);
     }
-    const int nch = std::max(1, (nt + 63) / 64);
-    std::vector<float4> clo(nch), chi(nch);
-    for (int j = 0; j < nch; j++) {
-      double lo[3] = {DBL_MAX, DBL_MAX, DBL_MAX}, hi[3] = {-DBL_MAX, -DBL_MAX, -DBL_MAX};
-      for (int k = 64 * j; k < std::min(nt, 64 * j + 64); k++) {
-        const double v[3] = {tv[k].x, tv[k].y, tv[k].z}, a[3] = {e1[k].x, e1[k].y, e1[k].z},
-                     b[3] = {e2[k].x, e2[k].y, e2[k].z};
-        for (int r = 0; r < 3; r++) {  // the triangle glm tests: v0 + u e1 + v e2, exact in double
-          lo[r] = std::min({lo[r], v[r], v[r] + a[r], v[r] + b[r]});
-          hi[r] = std::max({hi[r], v[r], v[r] + a[r], v[r] + b[r]});
-        }
-      }
-      float l[3], h[3];
-      for (int r = 0; r < 3; r++) {
-        if (lo[r] > hi[r]) lo[r] = hi[r] = 0.0;  // empty chunk (no triangles)
-        l[r] = (float)lo[r];
-        if ((double)l[r] > lo[r]) l[r] = std::nextafter(l[r], -FLT_MAX);
-        h[r] = (float)hi[r];
-        if ((double)h[r] < hi[r]) h[r] = std::nextafter(h[r], FLT_MAX);
-      }
-      clo[j] = make_float4(l[0], l[1], l[2], 0.0f);
-      chi[j] = make_float4(h[0], h[1], h[2], 0.0f);
-    }
+    std::vector<float4> clo, chi;
+    build_chunk_boxes(tv, e1, e2, nt, clo, chi);
+    set_cull(c, cluster_margin(tv, e1, e2));
     std::vector<BruteShape> shp(sc->num_shapes);
     for (int i = 0; i < sc->num_shapes; i++) {
       // glm::vec3(obj_polysbboxes[i] - 0.01, ...): double arithmetic, rounded to float by the constructor
@@ -2696,6 +2596,15 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     int rc = setup_trace(c);
     if (rc) return rc;
     if (c->grid_env) c->trace_grid = std::max(1, (int)(c->full_trace_grid * frac));
+  } else if (k == "cluster_cull") {
+    // 0: no cluster / chunk cull at all (every big-leaf cluster swept: exact by construction, whatever the
+    // scene's margin); 1: the scene's margin
+    if (v != 0) set_cull(c, c->cull);
+    else fix_cull(c, __builtin_inff());
+  } else if (k == "cull_margin") {
+    if (!(value >= 0.0)) return fail(KDPT_ERR_ARG, "cull_margin must be >= 0 (0: the scene's)");
+    if (value > 0.0) fix_cull(c, (float)value);
+    else set_cull(c, c->cull);
   } else if (k == "profile_batches") {
     c->profile_batches = v != 0;
     c->profile_steps = v >= 2;
@@ -2775,11 +2684,10 @@ int kdpt_trace_iteration(kdpt_ctx* c, int frame, int iter) {
   return KDPT_OK;
 }
 
-int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int stride, int pipeline, int batch) {
-  (void)frame;
-  if (!c || count < 0 || first_iter < 1 || stride < 1) return fail(KDPT_ERR_ARG, "bad arguments");
-  if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
-  HIP_TRY(hipSetDevice(c->device));
+// Iterations first_iter + k * stride (k < count) in batches of `batch`, `pipeline` batches in flight, their
+// partial images added into `target` (the context's image, or a frame buffer of kdpt_render_frames) in
+// iteration order on the accumulation stream.  Returns once everything is queued.
+int enqueue_iterations(kdpt_ctx* c, int first_iter, int count, int stride, int pipeline, int batch, float* target) {
   const int depth = std::min(16, std::max(1, pipeline));
   const int B = std::min(MAXB, std::max(1, batch));
   if (!c->accum_stream) HIP_TRY(hipStreamCreateWithFlags(&c->accum_stream, hipStreamNonBlocking));
@@ -2864,7 +2772,7 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
     PartialImages parts{};
     parts.nb = nb;
     for (int b = 0; b < nb; b++) parts.p[b] = grp[b]->image;  // in iteration order
-    hipLaunchKernelGGL(k_accumulate_batch, dim3((n3 + 255) / 256), dim3(256), 0, c->accum_stream, c->image, parts,
+    hipLaunchKernelGGL(k_accumulate_batch, dim3((n3 + 255) / 256), dim3(256), 0, c->accum_stream, target, parts,
                        n3);
     HIP_TRY(hipGetLastError());
     HIP_TRY(hipEventRecord(c->slot_free[g], c->accum_stream));
@@ -2872,6 +2780,14 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
   HIP_TRY(hipEventDestroy(entry));
   c->stats.iterations += count;
   return KDPT_OK;
+}
+
+int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int stride, int pipeline, int batch) {
+  (void)frame;
+  if (!c || count < 0 || first_iter < 1 || stride < 1) return fail(KDPT_ERR_ARG, "bad arguments");
+  if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
+  HIP_TRY(hipSetDevice(c->device));
+  return enqueue_iterations(c, first_iter, count, stride, pipeline, batch, c->image);
 }
 
 int kdpt_read_image(kdpt_ctx* c, float* rgb) {
@@ -2891,6 +2807,15 @@ int kdpt_trace_config(kdpt_ctx* c, int* tree_mode, int* block, int* grid, long l
     *block = m == TREE_LDS ? trace_block<TREE_LDS>() : (m >= TREE_LDS16 ? trace_block<TREE_LDS16>() : trace_block<TREE_PACKED>());
   if (grid) *grid = c->full_trace_grid;
   if (lds_bytes) *lds_bytes = (long long)c->tree_lds;
+  return KDPT_OK;
+}
+
+int kdpt_cull_margin(kdpt_ctx* c, float* margin, double* rigorous, int* exact) {
+  if (!c) return fail(KDPT_ERR_ARG, "null ctx");
+  if (margin) *margin = c->S.cl_margin;
+  if (rigorous) *rigorous = c->cull.rigorous;
+  // the box-only levels use cl_margin; the slab level's margin is rigorous by construction whenever that is
+  if (exact) *exact = (double)c->S.cl_margin >= c->cull.rigorous ? 1 : 0;
   return KDPT_OK;
 }
 
@@ -3000,6 +2925,9 @@ int kdpt_destroy(kdpt_ctx* c) {
   for (auto& evs : c->pending_ev)
     for (auto e : evs) (void)hipEventDestroy(e);
   for (auto e : c->free_ev) (void)hipEventDestroy(e);
+  release_comm(c);
+  for (auto e : c->frame_ev)
+    if (e) (void)hipEventDestroy(e);
   if (c->accum_stream) (void)hipStreamDestroy(c->accum_stream);
   if (c->accum_ev) (void)hipEventDestroy(c->accum_ev);
   for (void* p : c->allocs) (void)hipFree(p);
@@ -3495,3 +3423,294 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
 }
 
 }  // namespace
+
+// ---------------------------------------------------------------------------
+// Multi-GPU: samples per pixel sharded across GPUs (the reference renders one GPU's
+// iterations in pathtrace(), src/pathtrace.cu:2405-2635).  Frame f covers global iterations f * spp + 1 ..
+// (f + 1) * spp; rank r of N renders those with (iteration - 1 - f * spp) % N == r, in order, into its frame
+// buffer, and one reduce (sum, to rank 0) per frame combines them -- the path's only exchange step.  Every
+// iteration-dependent behaviour (RNG seeds, iteration 2's sort, cacherays) uses the global numbers.
+//
+// The reduce is RCCL's (ncclReduce over xGMI, one communicator rank per context; multi-process:
+// kdpt_comm_init, one process per GPU) or, inside one process (kdpt_render_sharded), either RCCL
+// (ncclCommInitAll) or a peer-copy reduce on device 0 that adds the ranks' frames in rank order (also usable
+// with several contexts on one device, which RCCL refuses).  RCCL is loaded at run time (dlopen): the library
+// has no link-time dependency on it, and a process that already holds it (torch) shares that copy.  All
+// reduces are queued on the accumulation streams, so frames stay in flight: frame f + 1's iterations run
+// while frame f is reduced.
+// ---------------------------------------------------------------------------
+namespace {
+
+struct Rccl {
+  ncclResult_t (*getUniqueId)(ncclUniqueId*);
+  ncclResult_t (*commInitRank)(ncclComm_t*, int, ncclUniqueId, int);
+  ncclResult_t (*commInitAll)(ncclComm_t*, int, const int*);
+  ncclResult_t (*commDestroy)(ncclComm_t);
+  ncclResult_t (*reduce)(const void*, void*, size_t, ncclDataType_t, ncclRedOp_t, int, ncclComm_t, hipStream_t);
+  ncclResult_t (*groupStart)();
+  ncclResult_t (*groupEnd)();
+  const char* (*errorString)(ncclResult_t);
+};
+
+const Rccl* rccl() {
+  static std::once_flag once;
+  static Rccl r{};
+  static bool ok = false;
+  std::call_once(once, [] {
+    void* h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+    if (!h) return;
+    r.getUniqueId = (decltype(r.getUniqueId))dlsym(h, "ncclGetUniqueId");
+    r.commInitRank = (decltype(r.commInitRank))dlsym(h, "ncclCommInitRank");
+    r.commInitAll = (decltype(r.commInitAll))dlsym(h, "ncclCommInitAll");
+    r.commDestroy = (decltype(r.commDestroy))dlsym(h, "ncclCommDestroy");
+    r.reduce = (decltype(r.reduce))dlsym(h, "ncclReduce");
+    r.groupStart = (decltype(r.groupStart))dlsym(h, "ncclGroupStart");
+    r.groupEnd = (decltype(r.groupEnd))dlsym(h, "ncclGroupEnd");
+    r.errorString = (decltype(r.errorString))dlsym(h, "ncclGetErrorString");
+    ok = r.getUniqueId && r.commInitRank && r.commInitAll && r.commDestroy && r.reduce && r.groupStart &&
+         r.groupEnd && r.errorString;
+  });
+  return ok ? &r : nullptr;
+}
+
+#define RCCL_TRY(R, x)                                                                 \
+  do {                                                                                 \
+    const ncclResult_t e_ = (x);                                                       \
+    if (e_ != ncclSuccess) return fail(KDPT_ERR_HIP, std::string("rccl: ") + (R)->errorString(e_)); \
+  } while (0)
+
+// frame image = a + b + ... (rank order), the copy-reduce's sum
+struct FrameParts {
+  const float* p[8];
+  int n;
+};
+__global__ void k_sum_frames(float* __restrict__ out, FrameParts parts, int n3) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= n3) return;
+  float v = parts.p[0][i];
+  for (int k = 1; k < parts.n; k++) v += parts.p[k][i];
+  out[i] = v;
+}
+
+void release_comm(kdpt_ctx* c) {
+  const Rccl* R = c->comm && c->owns_comm ? rccl() : nullptr;
+  if (R) (void)R->commDestroy((ncclComm_t)c->comm);
+  c->comm = nullptr;
+  c->owns_comm = false;
+}
+
+int frame_buffers(kdpt_ctx* c) {
+  const size_t n3 = 3 * (size_t)c->npix;
+  for (int k = 0; k < 2; k++) {
+    if (!c->frame_buf[k]) {
+      int rc = dalloc(c, &c->frame_buf[k], n3);
+      if (rc) return rc;
+      HIP_TRY(hipEventCreateWithFlags(&c->frame_ev[k], hipEventDisableTiming));
+      HIP_TRY(hipEventRecord(c->frame_ev[k], c->stream));
+    }
+  }
+  if (!c->frame_sum && c->rank == 0) return dalloc(c, &c->frame_sum, n3);
+  return KDPT_OK;
+}
+
+// Iterations of frame f for rank r of n: first, stride n, count.
+void frame_share(int f, int spp, int n, int r, int* first, int* count) {
+  *first = f * spp + 1 + r;
+  *count = r < spp ? (spp - r + n - 1) / n : 0;
+}
+
+// Queue frame f's share of this rank into frame_buf[f & 1] (zeroed first, after its previous reduce).
+int enqueue_frame(kdpt_ctx* c, int f, int spp, int pipeline, int batch) {
+  int rc = frame_buffers(c);
+  if (rc) return rc;
+  if (!c->accum_stream) HIP_TRY(hipStreamCreateWithFlags(&c->accum_stream, hipStreamNonBlocking));
+  float* fb = c->frame_buf[f & 1];
+  HIP_TRY(hipStreamWaitEvent(c->accum_stream, c->frame_ev[f & 1], 0));
+  HIP_TRY(hipMemsetAsync(fb, 0, sizeof(float) * 3 * (size_t)c->npix, c->accum_stream));
+  int first, count;
+  frame_share(f, spp, c->nranks, c->rank, &first, &count);
+  if (count > 0) rc = enqueue_iterations(c, first, count, c->nranks, pipeline, batch, fb);
+  return rc;
+}
+
+// Rank 0, after its frame image is in `sum`: add it into the context's image and copy it out.
+int finish_frame(kdpt_ctx* c, const float* sum, float* out, int k) {
+  const int n3 = 3 * c->npix;
+  PartialImages parts{};
+  parts.p[0] = sum;
+  parts.nb = 1;
+  hipLaunchKernelGGL(k_accumulate_batch, dim3((n3 + 255) / 256), dim3(256), 0, c->accum_stream, c->image, parts, n3);
+  HIP_TRY(hipGetLastError());
+  if (out)
+    HIP_TRY(hipMemcpyAsync(out + (size_t)k * n3, sum, sizeof(float) * n3, hipMemcpyDefault, c->accum_stream));
+  return KDPT_OK;
+}
+
+int check_frames_args(kdpt_ctx* c, int first_frame, int frames, int spp) {
+  if (!c || first_frame < 0 || frames < 0 || spp < 1) return fail(KDPT_ERR_ARG, "bad arguments");
+  if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
+  return KDPT_OK;
+}
+
+}  // namespace
+
+int kdpt_comm_unique_id(unsigned char* id) {
+  if (!id) return fail(KDPT_ERR_ARG, "null id");
+  const Rccl* R = rccl();
+  if (!R) return fail(KDPT_ERR_UNSUPPORTED, "librccl.so.1 not found");
+  static_assert(sizeof(ncclUniqueId) == KDPT_COMM_ID_BYTES, "ncclUniqueId size");
+  ncclUniqueId u;
+  RCCL_TRY(R, R->getUniqueId(&u));
+  memcpy(id, &u, sizeof u);
+  return KDPT_OK;
+}
+
+int kdpt_comm_init(kdpt_ctx* c, int nranks, int rank, const unsigned char* id) {
+  if (!c || nranks < 1 || rank < 0 || rank >= nranks) return fail(KDPT_ERR_ARG, "bad arguments");
+  if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
+  HIP_TRY(hipSetDevice(c->device));
+  int rc = kdpt_synchronize(c);
+  if (rc) return rc;
+  release_comm(c);
+  const Rccl* R = rccl();
+  c->nranks = nranks;
+  c->rank = rank;
+  c->external_reduce = nranks > 1 && !id;
+  if (nranks > 1 && id) {
+    if (!R) return fail(KDPT_ERR_UNSUPPORTED, "librccl.so.1 not found");
+    ncclUniqueId u;
+    memcpy(&u, id, sizeof u);
+    ncclComm_t comm;
+    RCCL_TRY(R, R->commInitRank(&comm, nranks, u, rank));
+    c->comm = comm;
+    c->owns_comm = true;
+  }
+  return KDPT_OK;
+}
+
+int kdpt_render_frames(kdpt_ctx* c, int first_frame, int frames, int spp, int pipeline, int batch, float* out) {
+  int rc = check_frames_args(c, first_frame, frames, spp);
+  if (rc) return rc;
+  HIP_TRY(hipSetDevice(c->device));
+  const Rccl* R = c->comm ? rccl() : nullptr;
+  if (c->nranks > 1 && !R && !c->external_reduce) return fail(KDPT_ERR_ARG, "kdpt_comm_init first");
+  const size_t n3 = 3 * (size_t)c->npix;
+  for (int k = 0; k < frames; k++) {
+    const int f = first_frame + k;
+    if ((rc = enqueue_frame(c, f, spp, pipeline, batch))) return rc;
+    float* fb = c->frame_buf[f & 1];
+    const float* sum = fb;
+    if (c->external_reduce) {  // the caller reduces: every rank's share goes out as it is
+      if (out)
+        HIP_TRY(hipMemcpyAsync(out + (size_t)k * n3, fb, sizeof(float) * n3, hipMemcpyDefault, c->accum_stream));
+      HIP_TRY(hipEventRecord(c->frame_ev[f & 1], c->accum_stream));
+      continue;
+    }
+    if (c->nranks > 1) {
+      RCCL_TRY(R, R->reduce(fb, c->rank == 0 ? c->frame_sum : nullptr, n3, ncclFloat32, ncclSum, 0,
+                            (ncclComm_t)c->comm, c->accum_stream));
+      sum = c->frame_sum;
+    }
+    if (c->rank == 0 && (rc = finish_frame(c, sum, out, k))) return rc;
+    HIP_TRY(hipEventRecord(c->frame_ev[f & 1], c->accum_stream));
+  }
+  return KDPT_OK;
+}
+
+int kdpt_render_sharded(const kdpt_scene* scene, const kdpt_options* opt, int ndev, const int* devices,
+                        int first_frame, int frames, int spp, int pipeline, int batch, int reduce, float* out) {
+  if (!scene || ndev < 1 || ndev > 8 || !devices || first_frame < 0 || frames < 0 || spp < 1 ||
+      (reduce != KDPT_REDUCE_RCCL && reduce != KDPT_REDUCE_COPY))
+    return fail(KDPT_ERR_ARG, "bad arguments");
+  kdpt_options o;
+  if (opt) o = *opt;
+  else kdpt_default_options(&o);
+  o.external_image = nullptr;
+  std::vector<kdpt_ctx*> cs(ndev, nullptr);
+  auto cleanup = [&](int rc) {
+    for (auto c : cs)
+      if (c) kdpt_destroy(c);  // (releases its communicator)
+    return rc;
+  };
+  int rc;
+  for (int i = 0; i < ndev; i++) {
+    if ((rc = kdpt_create(scene, &o, devices[i], &cs[i]))) return cleanup(rc);
+    cs[i]->nranks = ndev;
+    cs[i]->rank = i;
+  }
+  const Rccl* R = nullptr;
+  if (reduce == KDPT_REDUCE_RCCL) {
+    R = rccl();
+    if (!R) return cleanup(fail(KDPT_ERR_UNSUPPORTED, "librccl.so.1 not found"));
+    std::vector<ncclComm_t> comms(ndev);
+    const ncclResult_t e = R->commInitAll(comms.data(), ndev, devices);
+    if (e != ncclSuccess) return cleanup(fail(KDPT_ERR_HIP, std::string("rccl: ") + R->errorString(e)));
+    for (int i = 0; i < ndev; i++) {
+      cs[i]->comm = comms[i];
+      cs[i]->owns_comm = true;
+    }
+  }
+  kdpt_ctx* c0 = cs[0];
+  const int n3 = 3 * c0->npix;
+  std::vector<float*> staged(ndev, nullptr);  // copy-reduce: the other ranks' frames on device 0
+  if (reduce == KDPT_REDUCE_COPY)
+    for (int i = 1; i < ndev; i++)
+      if ((rc = dalloc(c0, &staged[i], (size_t)n3))) return cleanup(rc);
+  for (int k = 0; k < frames; k++) {
+    const int f = first_frame + k;
+    for (int i = 0; i < ndev; i++) {
+      if (hipSetDevice(cs[i]->device) != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "hipSetDevice"));
+      if ((rc = enqueue_frame(cs[i], f, spp, pipeline, batch))) return cleanup(rc);
+    }
+    if (hipSetDevice(c0->device) != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "hipSetDevice"));
+    if ((rc = frame_buffers(c0))) return cleanup(rc);
+    if (reduce == KDPT_REDUCE_RCCL) {
+      R->groupStart();
+      ncclResult_t e = ncclSuccess;
+      for (int i = 0; i < ndev && e == ncclSuccess; i++)
+        e = R->reduce(cs[i]->frame_buf[f & 1], i == 0 ? c0->frame_sum : nullptr, (size_t)n3, ncclFloat32, ncclSum,
+                      0, (ncclComm_t)cs[i]->comm, cs[i]->accum_stream);
+      const ncclResult_t e2 = R->groupEnd();
+      if (e != ncclSuccess || e2 != ncclSuccess)
+        return cleanup(fail(KDPT_ERR_HIP, std::string("rccl: ") + R->errorString(e != ncclSuccess ? e : e2)));
+    } else {
+      // device 0 waits for every rank's frame, copies the others' over (peer copies: xGMI between GPUs)
+      FrameParts parts{};
+      parts.n = ndev;
+      parts.p[0] = c0->frame_buf[f & 1];
+      for (int i = 1; i < ndev; i++) {
+        kdpt_ctx* ci = cs[i];
+        hipEvent_t ready;
+        if (hipSetDevice(ci->device) != hipSuccess || hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(ready, ci->accum_stream) != hipSuccess || hipSetDevice(c0->device) != hipSuccess ||
+            hipStreamWaitEvent(c0->accum_stream, ready, 0) != hipSuccess ||
+            hipMemcpyPeerAsync(staged[i], c0->device, ci->frame_buf[f & 1], ci->device, sizeof(float) * (size_t)n3,
+                               c0->accum_stream) != hipSuccess)
+          return cleanup(fail(KDPT_ERR_HIP, "copy reduce"));
+        (void)hipEventDestroy(ready);  // (released once recorded work completes)
+        parts.p[i] = staged[i];
+      }
+      hipLaunchKernelGGL(k_sum_frames, dim3((n3 + 255) / 256), dim3(256), 0, c0->accum_stream, c0->frame_sum, parts, n3);
+      if (hipGetLastError() != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "k_sum_frames"));
+      // the other ranks' frame_buf[f & 1] may be reused (frame f + 2) once these copies are done
+      for (int i = 1; i < ndev; i++) {
+        hipEvent_t done;
+        if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess ||
+            hipEventRecord(done, c0->accum_stream) != hipSuccess || hipSetDevice(cs[i]->device) != hipSuccess ||
+            hipStreamWaitEvent(cs[i]->accum_stream, done, 0) != hipSuccess || hipSetDevice(c0->device) != hipSuccess)
+          return cleanup(fail(KDPT_ERR_HIP, "copy reduce"));
+        (void)hipEventDestroy(done);
+      }
+    }
+    if ((rc = finish_frame(c0, c0->frame_sum, out, k))) return cleanup(rc);
+    for (int i = 0; i < ndev; i++) {
+      if (hipSetDevice(cs[i]->device) != hipSuccess ||
+          hipEventRecord(cs[i]->frame_ev[f & 1], cs[i]->accum_stream) != hipSuccess)
+        return cleanup(fail(KDPT_ERR_HIP, "hipEventRecord"));
+    }
+  }
+  for (int i = 0; i < ndev; i++)
+    if ((rc = kdpt_synchronize(cs[i]))) return cleanup(rc);
+  return cleanup(KDPT_OK);
+}

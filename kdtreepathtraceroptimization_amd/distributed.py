@@ -1,5 +1,9 @@
 """Samples-per-pixel sharding over ranks.
 
+Frames (kdpt_render_frames, bench.py): frame f covers global iterations f*spp + 1 .. (f+1)*spp; rank r of N
+renders those with (iteration - 1 - f*spp) % N == r (frame_share), and one reduce per frame combines the
+ranks' frame images -- weak scaling keeps spp = (per-GPU spp) * N, strong scaling a fixed spp.
+
 One process per GPU.  Rank r of N renders the global iterations 1 + k*N + r (k = 0, 1, ...), so every
 iteration-dependent behaviour of the reference -- the RNG seed makeSeededRandomEngine(iter, ...), the
 iteration-2 sort, cacherays -- sees the same global iteration number it would on one GPU.  Each rank
@@ -17,6 +21,18 @@ def global_iteration(step: int, world: int, rank: int) -> int:
 def shard_iterations(first_step: int, steps: int, world: int, rank: int) -> list:
     """The global iterations of local steps [first_step, first_step + steps) on `rank`."""
     return [global_iteration(s, world, rank) for s in range(first_step, first_step + steps)]
+
+
+def frame_share(frame: int, spp: int, world: int, rank: int):
+    """(first global iteration, count) of `rank`'s share of frame `frame` (stride `world`), as
+    kdpt_render_frames renders it."""
+    count = (spp - rank + world - 1) // world if rank < spp else 0
+    return frame * spp + 1 + rank, count
+
+
+def frame_iterations(frame: int, spp: int, world: int, rank: int) -> list:
+    first, count = frame_share(frame, spp, world, rank)
+    return [first + k * world for k in range(count)]
 
 
 def reduce_image(image, dist, dst: int = 0):

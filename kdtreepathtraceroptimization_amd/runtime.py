@@ -114,7 +114,10 @@ EXPORTS = [
     "kdpt_save_rgb8", "kdpt_save_png", "kdpt_save_hdr", "kdpt_png_encode", "kdpt_write_png", "kdpt_hdr_encode",
     "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm", "kdpt_set_options", "kdpt_scene_build_device",
     "kdpt_scene_kd_build_ms", "kdpt_build_kd_device", "kdpt_scene_load_device", "kdpt_trace_config",
+    "kdpt_cull_margin", "kdpt_comm_unique_id", "kdpt_comm_init", "kdpt_render_frames", "kdpt_render_sharded",
 ]
+
+REDUCE_RCCL, REDUCE_COPY = 0, 1  # kdpt_render_sharded's reduce (KDPT_REDUCE_*)
 
 _lib = None
 
@@ -156,6 +159,14 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_selftest_rng.argtypes = [P(C.c_int), C.c_int, C.c_int, P(C.c_float)]
     lib.kdpt_selftest_fresnel.argtypes = [P(C.c_float), C.c_int, C.c_float, P(C.c_float)]
     lib.kdpt_trace_config.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int), P(C.c_longlong)]
+    if hasattr(lib, "kdpt_cull_margin"):  # absent from older builds used in A/B runs
+        lib.kdpt_cull_margin.argtypes = [C.c_void_p, P(C.c_float), P(C.c_double), P(C.c_int)]
+    if hasattr(lib, "kdpt_render_frames"):
+        lib.kdpt_comm_unique_id.argtypes = [C.c_void_p]
+        lib.kdpt_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        lib.kdpt_render_frames.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
+        lib.kdpt_render_sharded.argtypes = [P(Scene), P(Options), C.c_int, P(C.c_int), C.c_int, C.c_int, C.c_int,
+                                            C.c_int, C.c_int, C.c_int, C.c_void_p]
     lib.kdpt_selftest_rng_draws.argtypes = [C.c_int, P(C.c_uint32), C.c_int, C.c_int, P(C.c_float)]
     if hasattr(lib, "kdpt_selftest_libm"):  # absent from older builds used in A/B runs
         lib.kdpt_selftest_libm.argtypes = [C.c_int, P(C.c_float), C.c_int, P(C.c_double)]
@@ -408,6 +419,21 @@ class PathTracer:
     def synchronize(self):
         _check(self.lib.kdpt_synchronize(self._ctx), "kdpt_synchronize")
 
+    def comm_init(self, nranks: int, rank: int, comm_id: Optional[bytes]):
+        """kdpt_comm_init: join an spp-sharded group (comm_id from comm_unique_id() on rank 0; None = no
+        communicator, render_frames hands each rank's frame shares out for the caller to reduce)."""
+        buf = None if comm_id is None else C.create_string_buffer(bytes(comm_id), COMM_ID_BYTES)
+        _check(self.lib.kdpt_comm_init(self._ctx, int(nranks), int(rank), buf), "kdpt_comm_init")
+
+    def render_frames(self, first_frame: int, frames: int, spp: int, pipeline: int = 8, batch: int = 8,
+                      out=None):
+        """kdpt_render_frames (async): this rank's share of frames of `spp` global iterations each, reduced
+        to rank 0 and added into its image; out: None, a device pointer (int) or a float32 numpy array of
+        frames * 3*W*H values (host copies complete at synchronize())."""
+        ptr = None if out is None else (int(out) if isinstance(out, int) else out.ctypes.data)
+        _check(self.lib.kdpt_render_frames(self._ctx, int(first_frame), int(frames), int(spp), int(pipeline),
+                                           int(batch), ptr), "kdpt_render_frames")
+
     def image(self) -> np.ndarray:
         out = np.empty((self.height, self.width, 3), dtype=np.float32)
         _check(self.lib.kdpt_read_image(self._ctx, _fptr(out)), "kdpt_read_image")
@@ -477,8 +503,17 @@ class PathTracer:
         m, b, g, l = C.c_int(), C.c_int(), C.c_int(), C.c_longlong()
         _check(self.lib.kdpt_trace_config(self._ctx, C.byref(m), C.byref(b), C.byref(g), C.byref(l)),
                "kdpt_trace_config")
-        return {"tree": self.TREE_MODES.get(m.value, str(m.value)), "block": b.value, "grid": g.value,
-                "lds_tree_bytes": l.value}
+        out = {"tree": self.TREE_MODES.get(m.value, str(m.value)), "block": b.value, "grid": g.value,
+               "lds_tree_bytes": l.value}
+        if hasattr(self.lib, "kdpt_cull_margin"):
+            out.update(self.cull_margin())
+        return out
+
+    def cull_margin(self) -> dict:
+        """kdpt_cull_margin: the cluster cull's margin coefficient, the scene's rigorous one, exact or not."""
+        k, r, e = C.c_float(), C.c_double(), C.c_int()
+        _check(self.lib.kdpt_cull_margin(self._ctx, C.byref(k), C.byref(r), C.byref(e)), "kdpt_cull_margin")
+        return {"cull_margin": k.value, "cull_rigorous": r.value, "cull_exact": bool(e.value)}
 
     def trace_grid_share(self) -> float:
         return float(self.stats().intersect_grid_share)
@@ -538,6 +573,33 @@ def imgsum(image: np.ndarray) -> float:
     im = np.asarray(image, dtype=np.float32).reshape(-1, 3)
     per_px = (im[:, 0] + im[:, 1]) + im[:, 2]  # float32 adds, left to right
     return float(np.sum(per_px.astype(np.float64)))
+
+
+COMM_ID_BYTES = 128
+
+
+def comm_unique_id() -> bytes:
+    """kdpt_comm_unique_id: the RCCL unique id rank 0 hands to every rank."""
+    lib = load_library()
+    buf = C.create_string_buffer(COMM_ID_BYTES)
+    _check(lib.kdpt_comm_unique_id(buf), "kdpt_comm_unique_id")
+    return buf.raw
+
+
+def render_sharded(scene: "SceneData", devices, first_frame: int, frames: int, spp: int,
+                   options: Optional[Options] = None, pipeline: int = 8, batch: int = 8,
+                   reduce: int = REDUCE_RCCL) -> np.ndarray:
+    """kdpt_render_sharded: one process, one context per device; returns the reduced frames
+    (frames, H, W, 3)."""
+    lib = load_library()
+    opt = options if options is not None else default_options()
+    devs = (C.c_int * len(devices))(*devices)
+    w, h = scene.resolution
+    out = np.zeros((frames, h, w, 3), dtype=np.float32)
+    _check(lib.kdpt_render_sharded(C.byref(scene.view), C.byref(opt), len(devices), devs, int(first_frame),
+                                   int(frames), int(spp), int(pipeline), int(batch), int(reduce),
+                                   out.ctypes.data), "kdpt_render_sharded")
+    return out
 
 
 def build_kd_device(verts9: np.ndarray, norms9: np.ndarray, mtl: np.ndarray, maxdepth: int = 13, device: int = 0):

@@ -67,3 +67,53 @@ def test_sharded_reduce_world2(tmp_path, oracle):
     assert np.array_equal(got.view(np.uint32), expect.view(np.uint32))
     seq = _render(range(1, world * STEPS + 1)).reshape(-1)
     assert np.allclose(got, seq, rtol=1e-5, atol=1e-5)
+
+
+def test_frame_shares_partition():
+    """kdpt_render_frames' split (distributed.frame_share, restated by the C++ frame_share): every global
+    iteration of a frame goes to exactly one rank, ranks take iterations f*F + 1 + r, stride N (strong and weak
+    scaling, frames larger and smaller than N)."""
+    from kdtreepathtraceroptimization_amd.distributed import frame_iterations, frame_share
+    for F in (1, 3, 8, 32, 256, 257):
+        for world in (1, 2, 3, 8):
+            for f in (0, 1, 5):
+                its = sorted(it for r in range(world) for it in frame_iterations(f, F, world, r))
+                assert its == list(range(f * F + 1, (f + 1) * F + 1)), (F, world, f)
+                counts = [frame_share(f, F, world, r)[1] for r in range(world)]
+                assert max(counts) - min(counts) <= 1
+
+
+def _frames_worker(rank, world, port, out, frames, F):
+    """bench.py's gloo branch: every rank renders its share of each frame, one reduce per frame, rank 0 adds
+    the reduced frames in order."""
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        from kdtreepathtraceroptimization_amd.distributed import frame_iterations
+        image = torch.zeros(3 * RES[0] * RES[1])
+        for f in range(frames):
+            share = torch.from_numpy(_render(frame_iterations(f, F, world, rank)).reshape(-1).copy())
+            dist.reduce(share, dst=0, op=dist.ReduceOp.SUM)
+            if rank == 0:
+                image += share
+        if rank == 0:
+            np.save(out, image.numpy())
+    finally:
+        dist.destroy_process_group()
+
+
+def test_frames_reduce_world2(tmp_path, oracle):
+    """Two gloo ranks, three 3-spp frames (odd: rank 0 takes two iterations, rank 1 one): equal to the same
+    grouping summed on one process, and to the sequential render within float summation order."""
+    from kdtreepathtraceroptimization_amd.distributed import frame_iterations
+    world, frames, F = 2, 3, 3
+    out = str(tmp_path / "img.npy")
+    mp.spawn(_frames_worker, args=(world, _free_port(), out, frames, F), nprocs=world, join=True)
+    got = np.load(out)
+    expect = np.zeros_like(got)
+    for f in range(frames):
+        parts = [_render(frame_iterations(f, F, world, r)).reshape(-1) for r in range(world)]
+        expect = expect + (parts[0] + parts[1])
+    assert np.array_equal(got.view(np.uint32), expect.view(np.uint32))
+    seq = _render(range(1, frames * F + 1)).reshape(-1)
+    assert np.allclose(got, seq, rtol=1e-5, atol=1e-5)

@@ -259,7 +259,8 @@ def test_pbo_into_device_memory(kdpt):
         assert np.array_equal(dev.cpu().numpy(), host)
 
 
-@pytest.mark.parametrize("pipeline,batch", [(1, 1), (3, 1), (2, 3), (1, 4), (8, 4), (5, 2), (12, 4), (3, 8), (8, 8), (2, 5)])
+@pytest.mark.parametrize("pipeline,batch", [(1, 1), (3, 1), (2, 3), (1, 4), (8, 4), (5, 2), (12, 4), (3, 8), (8, 8), (2, 5),
+                                            (2, 16), (8, 16), (3, 13)])
 def test_pipelined_iterations_bit_exact(kdpt, pipeline, batch):
     """kdpt_trace_iterations (batches sharing intersect launches, several batches in flight, partial
     images added in order) gives the same image bits and segment counts as one kdpt_trace_iteration
@@ -317,12 +318,40 @@ def test_tuning_knobs_keep_parity(kdpt):
             pt.set_tuning("no_such_knob", 1)
     for name, val in (("tree_global", 1), ("tree_format", 32), ("tree_format", 16), ("early_walk", 0), ("early_leaf", 65), ("chunk_width0", 64),
                       ("chunk_width1", 8), ("trace_grid_frac", 0.1), ("shade_fused", 0), ("shade_batch", 0),
-                      ("gen_geoms", 0)):
+                      ("gen_geoms", 0), ("cluster_cull", 0), ("cull_margin", 1e-3)):
         with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
             pt.set_tuning(name, val)
             pt.trace_iterations(1, 8, pipeline=2, batch=4)
             pt.synchronize()
             assert np.array_equal(pt.image().view(np.uint32), ref.view(np.uint32)), name
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mesh,res,depth,cap,iters", [("dragon_5", (800, 800), 8, 8, 16),
+                                                      ("icosphere_8", (1600, 1600), 16, 16, 2)])
+def test_cluster_cull_equals_no_cull_at_scale(kdpt, mesh, res, depth, cap, iters):
+    """The cluster cull (default margin) against no cull at all (tuning cluster_cull = 0: every cluster of
+    every visited big leaf swept, the reference's semantics by construction) on the headline workloads at
+    full size: C3 (dragon_5, 800^2, 16 iterations, ~40 M segments) and C5 (the 1.31 M-triangle icosphere,
+    1600^2, cap 16, 2 iterations, ~24 M segments).  Every ray of these renders is a differential case of the
+    cull: the images and segment counts must be bit-equal.  (C5's margin is the rigorous one, so this holds
+    for any ray there; dragon_5's triangles are too large for a rigorous margin that still culls --
+    kdpt_cull_margin reports exact = 0 -- and this shows the fast margin agrees on real rays.)"""
+    desc = load_fixture_scene("cornell", mesh, res=res, depth=depth)
+    sd = kdpt.SceneData.from_description(desc)
+    imgs, segs, info = [], [], None
+    for cull in (1, 0):
+        with kdpt.PathTracer(sd, kdpt.default_options(bounce_cap=cap)) as pt:
+            if info is None:
+                info = pt.cull_margin()
+            pt.set_tuning("cluster_cull", cull)
+            pt.trace_iterations(1, iters, pipeline=2, batch=2)
+            pt.synchronize()
+            imgs.append(pt.image())
+            segs.append(pt.stats().total_segments)
+    assert info["cull_exact"] == (mesh == "icosphere_8"), info
+    assert segs[0] == segs[1]
+    assert np.array_equal(imgs[0].view(np.uint32), imgs[1].view(np.uint32))
 
 
 @pytest.mark.parametrize("mesh,level,knobs,want", [("dragon_5", None, {"tree_format": 16}, "lds-16B-derived"),

@@ -79,17 +79,18 @@ def test_spp_sharded_world2_equals_oracle_grouping(tmp_path, oracle):
 
 def test_bench_main_world2_gloo(tmp_path):
     """bench.py's own N > 1 main(): two ranks launched by torch.distributed.run (sharing this box's one GPU,
-    so the framebuffer reduce goes through gloo; the driver's 8-GPU run takes the RCCL branch of the same
-    code), the stats all-reduces and the in-timed-region reduce.  The reduced image rank 0 dumps must equal
-    the two shards rendered here by the product one after the other and added (a + b is exact in either
-    order), and the segment count must be the shards' sum."""
+    so the frames are reduced over gloo from the shares kdpt_render_frames hands out; the driver's 8-GPU run
+    reduces inside libkdpt over RCCL instead), the stats all-reduces and the in-timed-region reduces.  The
+    image rank 0 dumps (the timed frames' reduced images added in frame order) must equal the product's own
+    renders of each rank's share of each frame, added rank by rank and frame by frame, and the segment count
+    must be the shares' sum."""
     import json
     import subprocess
     import sys
 
     from conftest import ROOT
     from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options
-    from kdtreepathtraceroptimization_amd.distributed import global_iteration
+    from kdtreepathtraceroptimization_amd.distributed import frame_share
 
     res, steps, warmup, spp, world = (160, 120), 2, 1, 4, 2
     out = str(tmp_path / "bench_img.npy")
@@ -101,15 +102,117 @@ def test_bench_main_world2_gloo(tmp_path):
     assert r.returncode == 0, r.stderr[-3000:]
     line = json.loads([x for x in r.stdout.splitlines() if x.startswith('{"metric"')][-1])
     assert line["n_gpus"] == world and line["steps"] == steps and line["value"] > 0
+    assert line["scaling"] == "weak" and line["config"]["spp_per_frame"] == spp * world
     got = np.load(out)
     sd = SceneData.from_description(load_fixture_scene("cornell", "dragon_5", res=res, depth=8))
-    parts, seg = [], 0
-    for rank in range(world):
-        with PathTracer(sd, default_options(testing_mode=1, short_stack=1, bounce_cap=8), device=0) as pt:
-            pt.trace_iterations(global_iteration(warmup * spp, world, rank), steps * spp, stride=world)
-            pt.synchronize()
-            parts.append(pt.image().reshape(-1))
-            seg += pt.stats().total_segments
-    assert line["segments_per_iteration"] * steps * spp * world == pytest.approx(seg, abs=1)
-    expect = parts[0] + parts[1]
+    F = spp * world
+    expect, seg = np.zeros(3 * res[0] * res[1], np.float32), 0
+    for f in range(warmup, warmup + steps):
+        parts = []
+        for rank in range(world):
+            first, count = frame_share(f, F, world, rank)
+            with PathTracer(sd, default_options(testing_mode=1, short_stack=1, bounce_cap=8), device=0) as pt:
+                pt.trace_iterations(first, count, stride=world, pipeline=2, batch=2)
+                pt.synchronize()
+                parts.append(pt.image().reshape(-1))
+                seg += pt.stats().total_segments
+        expect = expect + (parts[0] + parts[1])
+    assert line["segments_per_iteration"] * steps * F == pytest.approx(seg, abs=1)
     assert np.array_equal(got.view(np.uint32), expect.view(np.uint32)), f"{int(np.sum(got != expect))} differ"
+
+
+def test_bench_strong_scaling_world2_gloo(tmp_path):
+    """bench.py --total-spp (strong scaling, C4's shape): two ranks split each 6-spp frame 3 + 3; the line
+    says "strong" and the frame's per-GPU share, and the dumped image equals the shares added as above."""
+    import json
+    import subprocess
+    import sys
+
+    from conftest import ROOT
+    from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options
+    from kdtreepathtraceroptimization_amd.distributed import frame_share
+
+    res, steps, warmup, total, world = (128, 96), 2, 1, 6, 2
+    out = str(tmp_path / "bench_img.npy")
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={world}",
+           "--master-addr", "127.0.0.1", "--master-port", str(_free_port()), os.path.join(ROOT, "bench.py"),
+           "--gpus", str(world), "--dist-backend", "gloo", "--steps", str(steps), "--warmup", str(warmup),
+           "--total-spp", str(total), "--scene", "cornell8", "--res", *map(str, res), "--no-cpu-baseline",
+           "--dump-image", out]
+    r = subprocess.run(cmd, capture_output=True, text=True, timeout=240, cwd=ROOT)
+    assert r.returncode == 0, r.stderr[-3000:]
+    line = json.loads([x for x in r.stdout.splitlines() if x.startswith('{"metric"')][-1])
+    assert line["scaling"] == "strong" and line["config"]["spp_per_frame"] == total
+    assert line["config"]["spp_per_gpu_per_frame"] == total / world
+    sd = SceneData.from_description(load_fixture_scene("cornell8", "dragon_5", res=res, depth=8))
+    expect = np.zeros(3 * res[0] * res[1], np.float32)
+    for f in range(warmup, warmup + steps):
+        parts = []
+        for rank in range(world):
+            first, count = frame_share(f, total, world, rank)
+            with PathTracer(sd, default_options(testing_mode=1, short_stack=1, bounce_cap=8), device=0) as pt:
+                pt.trace_iterations(first, count, stride=world, pipeline=2, batch=2)
+                pt.synchronize()
+                parts.append(pt.image().reshape(-1))
+        expect = expect + (parts[0] + parts[1])
+    got = np.load(out)
+    assert np.array_equal(got.view(np.uint32), expect.view(np.uint32)), f"{int(np.sum(got != expect))} differ"
+
+
+# ---- the C-ABI's own multi-GPU entry points (kdpt_render_frames / kdpt_render_sharded) ----
+
+def _frame_parts(sd, frame, spp, world, **opt):
+    """Each rank's share of one frame, rendered alone by the product (iteration order)."""
+    from kdtreepathtraceroptimization_amd import PathTracer, default_options
+    parts = []
+    for r in range(world):
+        with PathTracer(sd, default_options(**opt), device=0) as pt:
+            first = frame * spp + 1 + r
+            count = (spp - r + world - 1) // world if r < spp else 0
+            if count:
+                pt.trace_iterations(first, count, stride=world, pipeline=2, batch=2)
+            pt.synchronize()
+            parts.append(pt.image())
+    return parts
+
+
+def test_render_frames_one_rank_equals_trace_iterations():
+    """kdpt_render_frames at one rank (no communicator): one frame into a zero image equals
+    kdpt_trace_iterations over the same iterations bit for bit, and frames f, f + 1 equal the two frame
+    images added in frame order; its `out` receives each frame."""
+    from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options
+    sd = SceneData.from_description(load_fixture_scene("cornell", "dragon_5", res=(200, 160), depth=8))
+    spp = 6
+    with PathTracer(sd, default_options(), device=0) as ref:
+        ref.trace_iterations(1, spp, pipeline=3, batch=2)
+        ref.synchronize()
+        one = ref.image()
+    with PathTracer(sd, default_options(), device=0) as pt:
+        out = np.zeros((2, 160, 200, 3), np.float32)
+        pt.render_frames(0, 2, spp, pipeline=3, batch=2, out=out)
+        pt.synchronize()
+        img = pt.image()
+    assert np.array_equal(out[0].view(np.uint32), one.view(np.uint32))
+    f1 = _frame_parts(sd, 1, spp, 1)[0]
+    assert np.array_equal(out[1].view(np.uint32), f1.view(np.uint32))
+    assert np.array_equal(img.view(np.uint32), (out[0] + out[1]).view(np.uint32))
+
+
+@pytest.mark.parametrize("reduce", ["copy", "rccl"])
+def test_render_sharded_equals_rank_parts(reduce):
+    """kdpt_render_sharded, one process, one context per device: with RCCL on this box's one GPU (one
+    rank: ncclCommInitAll + ncclReduce at N = 1) the frames equal kdpt_trace_iterations' renders; with the
+    in-process copy reduce the two "devices" are both cuda:0 (two contexts, which RCCL would refuse) and
+    each frame equals the two ranks' shares (global iterations f*spp + 1 + r, stride 2) added in rank order.
+    Iteration 2 (the sort) falls in frame 0's rank 1 share."""
+    from kdtreepathtraceroptimization_amd import SceneData
+    from kdtreepathtraceroptimization_amd.runtime import REDUCE_COPY, REDUCE_RCCL, render_sharded
+    sd = SceneData.from_description(load_fixture_scene("cornell8", "dragon_5", res=(160, 120), depth=8))
+    spp, frames = 5, 2
+    devices = [0, 0] if reduce == "copy" else [0]
+    got = render_sharded(sd, devices, 0, frames, spp, pipeline=2, batch=2,
+                         reduce=REDUCE_COPY if reduce == "copy" else REDUCE_RCCL)
+    for f in range(frames):
+        parts = _frame_parts(sd, f, spp, len(devices))
+        expect = parts[0] if len(parts) == 1 else parts[0] + parts[1]
+        assert np.array_equal(got[f].view(np.uint32), expect.view(np.uint32)), f"frame {f}"
