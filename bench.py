@@ -75,7 +75,7 @@ def parse():
     ap.add_argument("--cpu-iters", type=int, default=8, help="iterations per repeat of the multi-thread CPU leg")
     ap.add_argument("--pipeline", type=int, default=8,
                     help="batches in flight (kdpt_trace_iterations; bit-identical to one at a time)")
-    ap.add_argument("--batch", type=int, default=8, help="iterations sharing each intersect launch (<= MAXB)")
+    ap.add_argument("--batch", type=int, default=16, help="iterations sharing each intersect launch (<= MAXB = 16)")
     ap.add_argument("--force-dist", action="store_true",
                     help="run the process-group path (barriers, the in-timed-region reduce, stat all-reduces) even "
                          "with one rank, e.g. to exercise RCCL on a one-GPU box")

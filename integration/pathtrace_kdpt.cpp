@@ -4,8 +4,8 @@
 // else in the reference changes: Scene still parses the scene text, builds the KD tree on the host
 // (src/scene.cpp:866-968) and owns the arrays, which pass through as pointers (the layouts are the
 // reference's, include/kdpt.h).  tests/test_integration_shim.py compiles this file against include/kdpt.h
-// and a layout-identical stand-in of the reference's Scene (tests/native/shim_scene.h) and, on the GPU,
-// runs it against the C-ABI directly.
+// and a layout-identical stand-in of the reference's pathtrace.h / Scene (tests/native/shim/pathtrace.h)
+// and, on the GPU, runs it against the C-ABI directly.
 #include <cstdint>
 #include <cstdio>
 #include <cstdlib>

@@ -57,13 +57,13 @@ struct ClusterSet {
   std::vector<int2> leaf_cl, leaf_sp;  // per node: {first cluster, count} / {first super, count}
   std::vector<int4> sup;               // super-cluster records (DevScene::sup)
   std::vector<float4> lo, hi, nrm;     // cluster boxes (w: slab bounds) and slab normals
-  std::vector<float4> cv0, ce1, ce2;   // cluster-order triangles, 64 per cluster (ce1.w = original index)
+  std::vector<float4> cv0, ce1, ce2;   // cluster-order triangles, CLUSTER per cluster (ce1.w = original index)
   std::vector<int2> info;              // {first entry in cv0, triangle count}
   bool supers_finite = true;           // every super box is finite in half precision
 };
 
-// Big leaves as clusters of <= 64 triangles: Morton order of the triangle centroids inside the leaf's box,
-// consecutive runs of 64, each with its exact float box, the slab along its summed area vector, and runs of
+// Big leaves as clusters of <= CLUSTER triangles: Morton order of the triangle centroids inside the leaf's
+// box, consecutive runs of CLUSTER, each with its exact float box, the slab along its summed area vector, and runs of
 // SUPER clusters under one half-precision box rounded outward.
 inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tri_bare* tris,
                               const std::vector<float4>& tv, const std::vector<float4>& e1,
@@ -95,9 +95,9 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
     }
     std::stable_sort(key.begin(), key.end(), [](const std::pair<uint32_t, int>& a,
                                                 const std::pair<uint32_t, int>& b) { return a.first < b.first; });
-    cs.leaf_cl[i] = make_int2((int)cs.info.size(), (size + 63) / 64);
-    for (int b = 0; b < size; b += 64) {
-      const int cnt = std::min(64, size - b);
+    cs.leaf_cl[i] = make_int2((int)cs.info.size(), (size + CLUSTER - 1) / CLUSTER);
+    for (int b = 0; b < size; b += CLUSTER) {
+      const int cnt = std::min(CLUSTER, size - b);
       float l[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, h[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
       cs.info.push_back(make_int2((int)cs.cv0.size(), cnt));
       for (int k = b; k < b + cnt; k++) {
@@ -115,7 +115,7 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
         cs.ce1.push_back(q);
         cs.ce2.push_back(e2[t]);
       }
-      for (int k = cnt; k < 64; k++) {  // padding: e1 = e2 = 0 fails glm's determinant test
+      for (int k = cnt; k < CLUSTER; k++) {  // padding: e1 = e2 = 0 fails glm's determinant test
         cs.cv0.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));
         cs.ce1.push_back(make_float4(0.0f, 0.0f, 0.0f, ibits(-1)));
         cs.ce2.push_back(make_float4(0.0f, 0.0f, 0.0f, 0.0f));

@@ -108,7 +108,7 @@ struct DevScene {
   // big leaves (>= BIG_LEAF triangles) as clusters of <= 64 triangles in Morton order, each with its
   // box: leaf_cl[node] = {first cluster, count} (count 0: not big); cl_lo/cl_hi boxes; cl_info =
   // {first triangle, size}; cluster-order copies of v0/e1/e2 with the original index in e1.w, each
-  // cluster padded to 64 entries (cluster c = entries [64c, 64c + 64); padding: zeros, index -1)
+  // cluster padded to CLUSTER entries (cluster c = entries [CLUSTER c, CLUSTER (c + 1)); padding: zeros, index -1)
   const int2* leaf_cl;
   int num_clusters;
   const float4* cl_lo;
@@ -414,8 +414,13 @@ KDPT_HD int tri_test_v(const TriData& T, f3 o, f3 d, float& bx, float& by, float
 // one half-precision box.  The cluster cull below is host-compilable so that tests/native/cull_diff.cpp
 // can check it against tri_test_v on adversarial lines ("Cluster cull").
 // ---------------------------------------------------------------------------
+#ifndef KDPT_CLUSTER
+#define KDPT_CLUSTER 64  // tools/build_variant.sh experiments only (64 or 32)
+#endif
+constexpr int CLUSTER = KDPT_CLUSTER;  // triangles per cluster (a sweep tests 64 / CLUSTER clusters at once)
+static_assert(CLUSTER == 64 || CLUSTER == 32, "cluster size");
 #ifndef KDPT_SUPER
-#define KDPT_SUPER 16  // tools/build_variant.sh experiments only (a power of two <= 64)
+#define KDPT_SUPER (1024 / KDPT_CLUSTER)  // tools/build_variant.sh experiments only (a power of two <= 32)
 #endif
 constexpr int SUPER = KDPT_SUPER;  // clusters per super-cluster
 #ifndef KDPT_BIG_LEAF
@@ -1067,7 +1072,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     // Sweeps of the (ray, cluster) pairs `pass` marks: cluster c with the ray of lane own, each surviving
     // cluster by the whole wave, the next survivor's triangles fetched while this one is tested; the results
     // are folded into the owner lane's k_* (order-free).  Wave-uniform call.
-    auto sweep = [&](bool pass, int c, int own) {
+    auto sweep64 = [&](bool pass, int c, int own) {
       unsigned long long sm = __ballot(pass);
       int s = -1;
       TriData T{};
@@ -1128,7 +1133,100 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         T = Tn;
       }
     };
-    const int ncl = big ? (lsize + 63) >> 6 : 0;
+    // CLUSTER == 32: two (ray, cluster) pairs per round, lanes [0, 32) testing the first survivor's 32
+    // triangles with its ray and lanes [32, 64) the second's with its own; the results of each half are folded
+    // into that pair's owner lane as above (both halves may belong to one ray: the folds are order-free).
+    auto sweep32 = [&](bool pass, int c, int own) {
+      unsigned long long sm = __ballot(pass);
+      const bool hi = lane >= 32;
+      const unsigned long long hmask = hi ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+      auto take = [&]() {
+        int t = -1;
+        if (sm) {
+          t = __builtin_ctzll(sm);
+          sm &= sm - 1;
+        }
+        return t;
+      };
+      auto load = [&](int a, int b) {  // lane's half of survivors a (low) and b (high, -1: none)
+        const int ca = a >= 0 ? __builtin_amdgcn_readlane(c, a) : -1;
+        const int cb = b >= 0 ? __builtin_amdgcn_readlane(c, b) : -1;
+        const int mc = hi ? cb : ca;
+        TriData t{};  // zero edges fail glm's determinant test
+        if (mc >= 0) {
+          const int ct = mc * 32 + (lane & 31);
+          t = TriData{S.c_v0[ct], S.c_e1[ct], S.c_e2[ct]};
+        }
+        return t;
+      };
+      int s0 = take(), s1 = take();
+      TriData T{};
+      if (s0 >= 0) T = load(s0, s1);
+      while (s0 >= 0) {
+        const int n0 = take(), n1 = take();
+        TriData Tn{};
+        if (n0 >= 0) Tn = load(n0, n1);
+        if (COUNT) prof_add(WP, PROF_BIG_SWEEPS, 1);
+        const int j0 = __builtin_amdgcn_readlane(own, s0);
+        const int j1 = s1 >= 0 ? __builtin_amdgcn_readlane(own, s1) : j0;
+        const f3 o0 = mk3(readlane_f(o.x, j0), readlane_f(o.y, j0), readlane_f(o.z, j0));
+        const f3 d0 = mk3(readlane_f(d.x, j0), readlane_f(d.y, j0), readlane_f(d.z, j0));
+        const f3 o1 = mk3(readlane_f(o.x, j1), readlane_f(o.y, j1), readlane_f(o.z, j1));
+        const f3 d1 = mk3(readlane_f(d.x, j1), readlane_f(d.y, j1), readlane_f(d.z, j1));
+        const f3 jo = hi ? o1 : o0, jd = hi ? d1 : d0;
+        const int orig = fbits(T.e1.w);
+        float bx = 0, by = 0, bzk = 0;
+        const int r = tri_test_v(T, jo, jd, bx, by, bzk);
+        const unsigned long long m1 = __ballot(r >= 1);
+        if (COUNT && m1) {
+          prof_add(WP, PROF_BIG_PASS, 1);
+          prof_add(WP, PROF_BIG_MULTI, (m1 & (m1 - 1)) ? 1 : 0);
+        }
+        if (m1) {
+          const unsigned long long pk =
+              r >= 1 ? ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk) : 0ull;
+          const unsigned long long m2 = __ballot(r == 2);
+          unsigned long long key = ~0ull;
+          if (r == 2) {
+            f3 hp, nn;
+            const float t = tri_hit_t<HYBRID>(S, orig, jo, jd, bx, by, bzk, hp, nn);
+            if (t > 0.0f) key = ((unsigned long long)f2u(t) << 32) | (unsigned int)orig;
+          }
+#pragma unroll
+          for (int h = 0; h < 2; h++) {
+            const unsigned long long hm = h ? 0xffffffff00000000ull : 0x00000000ffffffffull;
+            const unsigned long long m1h = m1 & hm;
+            if (!m1h) continue;
+            const int jh = h ? j1 : j0;
+            const bool mine = (hm & hmask) != 0ull;  // this lane is in half h
+            const unsigned long long wm = (m1h & (m1h - 1)) == 0ull ? readlane_u64(pk, __builtin_ctzll(m1h))
+                                                                    : wave_max_u64(mine ? pk : 0ull);
+            if (lane == jh) k_pass = wm > k_pass ? wm : k_pass;
+            const unsigned long long m2h = m2 & hm;
+            if (m2h) {
+              const bool one = (m2h & (m2h - 1)) == 0ull;
+              const int lh2 = __builtin_ctzll(m2h);
+              const int lh = one ? __builtin_amdgcn_readlane(orig, lh2)
+                                 : wave_max_i32(mine && r == 2 ? orig : -1);
+              const unsigned long long wb = one ? readlane_u64(key, lh2) : wave_min_u64(mine ? key : ~0ull);
+              if (lane == jh) {
+                k_nhit += __builtin_popcountll(m2h);
+                k_lasthit = max(k_lasthit, lh);
+                k_best = wb < k_best ? wb : k_best;
+              }
+            }
+          }
+        }
+        s0 = n0;
+        s1 = n1;
+        T = Tn;
+      }
+    };
+    auto sweep = [&](bool pass, int c, int own) {
+      if constexpr (CLUSTER == 32) sweep32(pass, c, own);
+      else sweep64(pass, c, own);
+    };
+    const int ncl = big ? (lsize + CLUSTER - 1) / CLUSTER : 0;
     if constexpr (ClusterSrc::kSuper) {
       // Two levels (leaves of thousands of triangles, e.g. the C5 icosphere's): the (ray, super-cluster) pairs
       // are culled first, 64 per pass, against the supers' boxes (LDS); each surviving super's SUPER clusters

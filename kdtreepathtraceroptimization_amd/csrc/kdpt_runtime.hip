@@ -2825,10 +2825,11 @@ int kdpt_write_pbo(kdpt_ctx* c, int iter, uint8_t* rgba) {
   int rc = join_accum(c);
   if (rc) return rc;
   // The reference's pbo is the GL-mapped device buffer (src/main.cpp runCuda); a headless caller passes host
-  // memory.  Device memory (of any device: peer access) is written by the kernel directly, anything else
-  // through the context's staging buffer.
+  // memory.  Memory of this context's device is written by the kernel directly; anything else (host memory,
+  // another device's buffer) through the context's staging buffer and a copy.
   hipPointerAttribute_t attr{};
-  const bool on_device = hipPointerGetAttributes(&attr, rgba) == hipSuccess && attr.type == hipMemoryTypeDevice;
+  const bool on_device = hipPointerGetAttributes(&attr, rgba) == hipSuccess && attr.type == hipMemoryTypeDevice &&
+                         attr.device == c->device;
   (void)hipGetLastError();  // a plain host pointer is an error for hipPointerGetAttributes on some runtimes
   uchar4* d = reinterpret_cast<uchar4*>(rgba);
   if (!on_device) {
@@ -2838,7 +2839,7 @@ int kdpt_write_pbo(kdpt_ctx* c, int iter, uint8_t* rgba) {
   hipLaunchKernelGGL(k_pbo, dim3((c->npix + 255) / 256), dim3(256), 0, c->stream, c->image, c->npix, iter, d);
   HIP_TRY(hipGetLastError());
   if (!on_device)
-    HIP_TRY(hipMemcpyAsync(rgba, d, sizeof(uchar4) * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
+    HIP_TRY(hipMemcpyAsync(rgba, d, sizeof(uchar4) * (size_t)c->npix, hipMemcpyDefault, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return KDPT_OK;
 }

@@ -210,9 +210,11 @@ RNG_MODES = ("seeded", "camera", "raw")
 def rng_host():
     exe = os.path.join(ROOT, "build", "rng_host")
     os.makedirs(os.path.dirname(exe), exist_ok=True)
+    tmp = exe + f".{os.getpid()}"  # parallel workers may be running the previous one
     subprocess.run(["g++", "-O2", "-std=c++17", "-ffp-contract=off", "-fno-fast-math", "-I",
-                    os.path.join(ROOT, "include"), os.path.join(TESTS, "native", "rng_host.cpp"), "-o", exe],
+                    os.path.join(ROOT, "include"), os.path.join(TESTS, "native", "rng_host.cpp"), "-o", tmp],
                    check=True)
+    os.replace(tmp, exe)
     return exe
 
 
