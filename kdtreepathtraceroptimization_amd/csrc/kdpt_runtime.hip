@@ -1720,6 +1720,7 @@ struct kdpt_ctx {
   kdpt_ctx* parent = nullptr;
   std::vector<kdpt_ctx*> slots;
   int slot_batch = 1;
+  int next_group = 0;  // the slot group the next batch goes to
   bool profile_batches = false;
   bool profile_steps = false;  // "profile_batches" = 2
   std::vector<hipEvent_t> slot_done, slot_free;
@@ -1747,7 +1748,9 @@ struct kdpt_ctx {
   bool external_reduce = false;  // kdpt_comm_init without an id: each rank hands its frame shares out
   float* frame_buf[2] = {nullptr, nullptr};
   float* frame_sum = nullptr;
-  hipEvent_t frame_ev[2] = {nullptr, nullptr};  // frame_buf[k] consumed by its reduce (copy-reduce mode)
+  hipEvent_t frame_ev[2] = {nullptr, nullptr};      // frame_buf[k] consumed by its reduce
+  hipEvent_t frame_acc_ev[2] = {nullptr, nullptr};  // frame_buf[k]'s accumulations done
+  hipStream_t reduce_stream = nullptr;  // the frames' reduces and image adds, beside the accumulation stream
 };
 
 namespace {
@@ -2710,6 +2713,7 @@ int enqueue_iterations(kdpt_ctx* c, int first_iter, int count, int stride, int p
       c->slot_free.clear();
     }
     c->slot_batch = B;
+    c->next_group = 0;
     // Only the group leaders create streams, one after another: HIP maps streams onto its hardware queues
     // (GPU_MAX_HW_QUEUES) in creation order, reusing the least-used queue once all exist, so a stream per
     // slot context (8 x 4) had put pairs of leaders -- two batches' chains -- on one in-order queue.
@@ -2741,9 +2745,12 @@ int enqueue_iterations(kdpt_ctx* c, int first_iter, int count, int stride, int p
       c->slots.empty() ? 1.0f : (float)c->slots[0]->trace_grid / (float)std::max(1, c->full_trace_grid);
   // diagnostic ("profile_batches" knob): the counting intersect kernel (kdpt_wave_profile after sync)
   if (c->profile_batches) HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(Counters), c->stream));
-  for (int kb = 0, bi = 0; kb < count; kb += B, bi++) {
+  for (int kb = 0; kb < count; kb += B) {
     const int nb = std::min(B, count - kb);
-    const int g = bi % ngroups;
+    // groups in turn, continuing across calls: kdpt_render_frames queues one call per frame, and a frame
+    // shorter than the pipeline must not restart at group 0 (it would wait on that group's previous batch)
+    const int g = c->next_group % ngroups;
+    c->next_group = (g + 1) % ngroups;
     kdpt_ctx* const* grp = &c->slots[(size_t)g * B];
     hipStream_t st = grp[0]->stream;
     HIP_TRY(hipStreamWaitEvent(st, c->slot_free[g], 0));  // the group's last partial images were consumed
@@ -2927,8 +2934,12 @@ int kdpt_destroy(kdpt_ctx* c) {
     for (auto e : evs) (void)hipEventDestroy(e);
   for (auto e : c->free_ev) (void)hipEventDestroy(e);
   release_comm(c);
+  if (c->reduce_stream) (void)hipStreamSynchronize(c->reduce_stream);
   for (auto e : c->frame_ev)
     if (e) (void)hipEventDestroy(e);
+  for (auto e : c->frame_acc_ev)
+    if (e) (void)hipEventDestroy(e);
+  if (c->reduce_stream) (void)hipStreamDestroy(c->reduce_stream);
   if (c->accum_stream) (void)hipStreamDestroy(c->accum_stream);
   if (c->accum_ev) (void)hipEventDestroy(c->accum_ev);
   for (void* p : c->allocs) (void)hipFree(p);
@@ -3503,11 +3514,13 @@ void release_comm(kdpt_ctx* c) {
 
 int frame_buffers(kdpt_ctx* c) {
   const size_t n3 = 3 * (size_t)c->npix;
+  if (!c->reduce_stream) HIP_TRY(hipStreamCreateWithFlags(&c->reduce_stream, hipStreamNonBlocking));
   for (int k = 0; k < 2; k++) {
     if (!c->frame_buf[k]) {
       int rc = dalloc(c, &c->frame_buf[k], n3);
       if (rc) return rc;
       HIP_TRY(hipEventCreateWithFlags(&c->frame_ev[k], hipEventDisableTiming));
+      HIP_TRY(hipEventCreateWithFlags(&c->frame_acc_ev[k], hipEventDisableTiming));
       HIP_TRY(hipEventRecord(c->frame_ev[k], c->stream));
     }
   }
@@ -3536,15 +3549,14 @@ int enqueue_frame(kdpt_ctx* c, int f, int spp, int pipeline, int batch) {
 }
 
 // Rank 0, after its frame image is in `sum`: add it into the context's image and copy it out.
-int finish_frame(kdpt_ctx* c, const float* sum, float* out, int k) {
+int finish_frame(kdpt_ctx* c, const float* sum, float* out, int k, hipStream_t st) {
   const int n3 = 3 * c->npix;
   PartialImages parts{};
   parts.p[0] = sum;
   parts.nb = 1;
-  hipLaunchKernelGGL(k_accumulate_batch, dim3((n3 + 255) / 256), dim3(256), 0, c->accum_stream, c->image, parts, n3);
+  hipLaunchKernelGGL(k_accumulate_batch, dim3((n3 + 255) / 256), dim3(256), 0, st, c->image, parts, n3);
   HIP_TRY(hipGetLastError());
-  if (out)
-    HIP_TRY(hipMemcpyAsync(out + (size_t)k * n3, sum, sizeof(float) * n3, hipMemcpyDefault, c->accum_stream));
+  if (out) HIP_TRY(hipMemcpyAsync(out + (size_t)k * n3, sum, sizeof(float) * n3, hipMemcpyDefault, st));
   return KDPT_OK;
 }
 
@@ -3601,21 +3613,27 @@ int kdpt_render_frames(kdpt_ctx* c, int first_frame, int frames, int spp, int pi
     const int f = first_frame + k;
     if ((rc = enqueue_frame(c, f, spp, pipeline, batch))) return rc;
     float* fb = c->frame_buf[f & 1];
+    // the frame's reduce and image add run on the reduce stream once its accumulations are done, while the
+    // accumulation stream goes on with the next frame's (other buffer)
+    const hipStream_t rs = c->reduce_stream;
+    HIP_TRY(hipEventRecord(c->frame_acc_ev[f & 1], c->accum_stream));
+    HIP_TRY(hipStreamWaitEvent(rs, c->frame_acc_ev[f & 1], 0));
     const float* sum = fb;
     if (c->external_reduce) {  // the caller reduces: every rank's share goes out as it is
-      if (out)
-        HIP_TRY(hipMemcpyAsync(out + (size_t)k * n3, fb, sizeof(float) * n3, hipMemcpyDefault, c->accum_stream));
-      HIP_TRY(hipEventRecord(c->frame_ev[f & 1], c->accum_stream));
-      continue;
+      if (out) HIP_TRY(hipMemcpyAsync(out + (size_t)k * n3, fb, sizeof(float) * n3, hipMemcpyDefault, rs));
+    } else {
+      if (c->nranks > 1) {
+        RCCL_TRY(R, R->reduce(fb, c->rank == 0 ? c->frame_sum : nullptr, n3, ncclFloat32, ncclSum, 0,
+                              (ncclComm_t)c->comm, rs));
+        sum = c->frame_sum;
+      }
+      if (c->rank == 0 && (rc = finish_frame(c, sum, out, k, rs))) return rc;
     }
-    if (c->nranks > 1) {
-      RCCL_TRY(R, R->reduce(fb, c->rank == 0 ? c->frame_sum : nullptr, n3, ncclFloat32, ncclSum, 0,
-                            (ncclComm_t)c->comm, c->accum_stream));
-      sum = c->frame_sum;
-    }
-    if (c->rank == 0 && (rc = finish_frame(c, sum, out, k))) return rc;
-    HIP_TRY(hipEventRecord(c->frame_ev[f & 1], c->accum_stream));
+    HIP_TRY(hipEventRecord(c->frame_ev[f & 1], rs));
   }
+  // whatever follows on the accumulation stream (the next call's accumulations, kdpt_synchronize, entry
+  // points that read the image) follows the last reduce too
+  if (frames > 0) HIP_TRY(hipStreamWaitEvent(c->accum_stream, c->frame_ev[(first_frame + frames - 1) & 1], 0));
   return KDPT_OK;
 }
 
@@ -3704,7 +3722,7 @@ int kdpt_render_sharded(const kdpt_scene* scene, const kdpt_options* opt, int nd
         (void)hipEventDestroy(done);
       }
     }
-    if ((rc = finish_frame(c0, c0->frame_sum, out, k))) return cleanup(rc);
+    if ((rc = finish_frame(c0, c0->frame_sum, out, k, c0->accum_stream))) return cleanup(rc);
     for (int i = 0; i < ndev; i++) {
       if (hipSetDevice(cs[i]->device) != hipSuccess ||
           hipEventRecord(cs[i]->frame_ev[f & 1], cs[i]->accum_stream) != hipSuccess)

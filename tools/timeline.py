@@ -18,6 +18,7 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("csv")
     ap.add_argument("--last-ms", type=float, default=30.0)
+    ap.add_argument("--shares", type=int, default=4, help="k_trace launches that fill the chip (1 / grid share)")
     a = ap.parse_args()
     rows = list(csv.DictReader(open(a.csv)))
     ev = []
@@ -41,6 +42,8 @@ def main():
     acc = defaultdict(float)
     acc_wg = defaultdict(float)
     idle = 0.0
+    starved = 0.0   # fewer k_trace launches in flight than fill the chip, while shading runs
+    exposed = 0.0   # no k_trace at all in flight, while shading runs
     hist = defaultdict(float)
     last = t0
     for t, d, n, nwg in pts:
@@ -54,6 +57,11 @@ def main():
             for k, v in cur_wg.items():
                 acc_wg[k] += v * dt
             hist[cur.get("k_trace", 0)] += dt
+            shading = cur.get("k_shade_fused_b", 0) + cur.get("k_shade_fused", 0) + cur.get("k_shade", 0)
+            if shading > 0 and cur.get("k_trace", 0) < a.shares:
+                starved += dt
+            if shading > 0 and cur.get("k_trace", 0) == 0:
+                exposed += dt
             last = t
         cur[n] += d
         cur_wg[n] += d * nwg
@@ -62,6 +70,9 @@ def main():
     for k in sorted(acc, key=lambda k: -acc[k]):
         print(f"{k:24s} avg in flight {acc[k] / span:6.2f}   avg workgroups {acc_wg[k] / span:9.1f}")
     print("k_trace launches in flight: " + ", ".join(f"{k}: {v / span:.3f}" for k, v in sorted(hist.items())))
+    # shading on the critical path: time in which a batch's shading runs while k_trace does not fill the chip
+    # (fewer than --shares launches in flight), and while no k_trace runs at all
+    print(f"shading with k_trace under {a.shares} launches: {starved / span:.4f}; with no k_trace: {exposed / span:.4f}")
 
 
 if __name__ == "__main__":
