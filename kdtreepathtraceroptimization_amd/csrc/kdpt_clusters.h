@@ -57,6 +57,7 @@ struct ClusterSet {
   std::vector<int2> leaf_cl, leaf_sp;  // per node: {first cluster, count} / {first super, count}
   std::vector<int4> sup;               // super-cluster records (DevScene::sup)
   std::vector<float4> lo, hi, nrm;     // cluster boxes (w: slab bounds) and slab normals
+  std::vector<float4> obb_u, obb_v, obb_w;  // the patch's in-plane slabs (DevScene::cl_u, cl_v, cl_w)
   std::vector<float4> cv0, ce1, ce2;   // cluster-order triangles, CLUSTER per cluster (ce1.w = original index)
   std::vector<int2> info;              // {first entry in cv0, triangle count}
   bool supers_finite = true;           // every super box is finite in half precision
@@ -174,6 +175,62 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
       cs.lo.push_back(make_float4(l[0], l[1], l[2], dlo));
       cs.hi.push_back(make_float4(h[0], h[1], h[2], dhi));
       cs.nrm.push_back(make_float4(nf[0], nf[1], nf[2], sf));
+      // the oriented box's in-plane directions: u along the principal axis of the vertices projected on
+      // the plane, v = n x u (any unit directions would be valid slabs; these make the box tight), the
+      // bounds of u . (q - c), v . (q - c) over the vertices in double, rounded outward to float
+      float uf[3] = {0.0f, 0.0f, 0.0f}, vf[3] = {0.0f, 0.0f, 0.0f};
+      float ulo = -FLT_MAX, uhi = FLT_MAX, vlo = -FLT_MAX, vhi = FLT_MAX;
+      if (nl > 0 && std::isfinite(nl)) {
+        const double n3[3] = {ns[0] / nl, ns[1] / nl, ns[2] / nl};
+        const int amin = std::fabs(n3[0]) <= std::fabs(n3[1]) && std::fabs(n3[0]) <= std::fabs(n3[2]) ? 0
+                         : (std::fabs(n3[1]) <= std::fabs(n3[2]) ? 1 : 2);
+        const double ax[3] = {amin == 0 ? 1.0 : 0.0, amin == 1 ? 1.0 : 0.0, amin == 2 ? 1.0 : 0.0};
+        double e1[3] = {n3[1] * ax[2] - n3[2] * ax[1], n3[2] * ax[0] - n3[0] * ax[2], n3[0] * ax[1] - n3[1] * ax[0]};
+        const double e1l = std::sqrt(e1[0] * e1[0] + e1[1] * e1[1] + e1[2] * e1[2]);
+        for (double& x : e1) x /= e1l;
+        const double e2[3] = {n3[1] * e1[2] - n3[2] * e1[1], n3[2] * e1[0] - n3[0] * e1[2], n3[0] * e1[1] - n3[1] * e1[0]};
+        double sx = 0, sy = 0, sxx = 0, syy = 0, sxy = 0;
+        int cntv = 0;
+        for (int k = b; k < b + cnt; k++) {
+          const kdpt_tri_bare& T = tris[start + key[k].second];
+          const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
+          for (int q = 0; q < 3; q++) {
+            const double p[3] = {(double)vx[q] - cc[0], (double)vy[q] - cc[1], (double)vz[q] - cc[2]};
+            const double x = e1[0] * p[0] + e1[1] * p[1] + e1[2] * p[2], y = e2[0] * p[0] + e2[1] * p[1] + e2[2] * p[2];
+            sx += x; sy += y; sxx += x * x; syy += y * y; sxy += x * y;
+            cntv++;
+          }
+        }
+        const double mx = sx / cntv, my = sy / cntv;
+        const double cxx = sxx / cntv - mx * mx, cyy = syy / cntv - my * my, cxy = sxy / cntv - mx * my;
+        const double th = 0.5 * std::atan2(2.0 * cxy, cxx - cyy);
+        const double ud[3] = {std::cos(th) * e1[0] + std::sin(th) * e2[0], std::cos(th) * e1[1] + std::sin(th) * e2[1],
+                              std::cos(th) * e1[2] + std::sin(th) * e2[2]};
+        const double vd[3] = {n3[1] * ud[2] - n3[2] * ud[1], n3[2] * ud[0] - n3[0] * ud[2], n3[0] * ud[1] - n3[1] * ud[0]};
+        for (int a = 0; a < 3; a++) {
+          uf[a] = (float)ud[a];
+          vf[a] = (float)vd[a];
+        }
+        double umn = 1e300, umx = -1e300, vmn = 1e300, vmx = -1e300;
+        for (int k = b; k < b + cnt; k++) {
+          const kdpt_tri_bare& T = tris[start + key[k].second];
+          const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
+          for (int q = 0; q < 3; q++) {
+            const double p[3] = {(double)vx[q] - cc[0], (double)vy[q] - cc[1], (double)vz[q] - cc[2]};
+            const double du = (double)uf[0] * p[0] + (double)uf[1] * p[1] + (double)uf[2] * p[2];
+            const double dv = (double)vf[0] * p[0] + (double)vf[1] * p[1] + (double)vf[2] * p[2];
+            umn = std::min(umn, du); umx = std::max(umx, du);
+            vmn = std::min(vmn, dv); vmx = std::max(vmx, dv);
+          }
+        }
+        ulo = std::nextafter((float)umn, -FLT_MAX);
+        uhi = std::nextafter((float)umx, FLT_MAX);
+        vlo = std::nextafter((float)vmn, -FLT_MAX);
+        vhi = std::nextafter((float)vmx, FLT_MAX);
+      }
+      cs.obb_u.push_back(make_float4(uf[0], uf[1], uf[2], ulo));
+      cs.obb_v.push_back(make_float4(vf[0], vf[1], vf[2], vlo));
+      cs.obb_w.push_back(make_float4(uhi, vhi, 0.0f, 0.0f));
     }
     const int c0 = cs.leaf_cl[i].x, ncl = cs.leaf_cl[i].y;
     cs.leaf_sp[i] = make_int2((int)cs.sup.size(), (ncl + SUPER - 1) / SUPER);

@@ -125,6 +125,14 @@ struct DevScene {
   // The two-level cull tests the line against this slab as well as the box (knob "cluster_slab")
   const float4* cl_n;
   int cl_slab;
+  // ... and the patch's extent along two unit directions u, v in its plane (u: the principal axis of its
+  // vertices projected on the plane, v = n x u): cl_u = (u, min u.(q - c)), cl_v = (v, min v.(q - c)),
+  // cl_w = (max u.(q - c), max v.(q - c), -, -), bounds rounded outward; with the slab an oriented box the
+  // second cull level tests when cl_obb is set (knob "cluster_obb")
+  const float4* cl_u;
+  const float4* cl_v;
+  const float4* cl_w;
+  int cl_obb;
   // the cull's margin coefficients (kdpt_clusters.h cluster_margin): cl_margin for the box-only tests;
   // the slab level uses cull_margin_dir(): max(cl_margin_lo, min(cl_margin, cull_a / g + cull_c)),
   // g = |n . d| - cl_n.w - cull_b
@@ -505,6 +513,37 @@ KDPT_HD bool cluster_may_pass_slab(float4 lo, float4 hi, float4 n, f3 o, f3 inv,
   return tmin <= tmax;
 }
 
+// cluster_may_pass_slab and the patch's u and v slabs: the line's interval through the cluster's oriented box
+// (n, u, v) must meet its interval through the axis-aligned one, every slab widened by the same margin.  A
+// point the float u/v tests accept lies within the margin of the line and inside every one of them, so the
+// cull stays as conservative as the box alone.
+KDPT_HD void slab_clip(float lo, float hi, float m, float sd, float so, float& tmin, float& tmax) {
+  if (fabsf(sd) > 1e-12f) {
+    const float rs = 1.0f / sd;
+    const float s1 = (lo - m - so) * rs, s2 = (hi + m - so) * rs;
+    tmin = fmaxf(tmin, fminf(s1, s2));
+    tmax = fminf(tmax, fmaxf(s1, s2));
+  }
+}
+KDPT_HD bool cluster_may_pass_obb(float4 lo, float4 hi, float4 n, float4 u, float4 v, float4 w, f3 o, f3 inv, f3 d,
+                                  const CullK& k) {
+  const float nd = n.x * d.x + n.y * d.y + n.z * d.z;
+  const float K = cull_margin_dir(nd, n.w, k);
+  const float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
+  const float m = K * (1.0f + fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) + (hi.x - lo.x) +
+                           (hi.y - lo.y) + (hi.z - lo.z));
+  const float t1x = (lo.x - m - o.x) * inv.x, t2x = (hi.x + m - o.x) * inv.x;
+  const float t1y = (lo.y - m - o.y) * inv.y, t2y = (hi.y + m - o.y) * inv.y;
+  const float t1z = (lo.z - m - o.z) * inv.z, t2z = (hi.z + m - o.z) * inv.z;
+  float tmin = fmaxf(fmaxf(fminf(t1x, t2x), fminf(t1y, t2y)), fminf(t1z, t2z));
+  float tmax = fminf(fminf(fmaxf(t1x, t2x), fmaxf(t1y, t2y)), fmaxf(t1z, t2z));
+  const float ox = o.x - cx, oy = o.y - cy, oz = o.z - cz;
+  slab_clip(lo.w, hi.w, m, nd, n.x * ox + n.y * oy + n.z * oz, tmin, tmax);
+  slab_clip(u.w, w.x, m, u.x * d.x + u.y * d.y + u.z * d.z, u.x * ox + u.y * oy + u.z * oz, tmin, tmax);
+  slab_clip(v.w, w.y, m, v.x * d.x + v.y * d.y + v.z * d.z, v.x * ox + v.y * oy + v.z * oz, tmin, tmax);
+  return tmin <= tmax;
+}
+
 #if defined(__HIPCC__) || defined(__HIP__)
 // ---------------------------------------------------------------------------
 // Wave-cooperative form of traverseKD for gfx950 (64-lane waves).
@@ -686,6 +725,9 @@ struct ClustersSuper {
   const float4* lo;
   const float4* hi;
   const float4* n;  // slab normals (DevScene::cl_n)
+  const float4* u;  // the oriented box's in-plane slabs (DevScene::cl_u, cl_v, cl_w)
+  const float4* v;
+  const float4* w;
   __device__ float4 n_of(int c) const { return n[c]; }
   // box of super k, and its first cluster << 5 | count - 1
   __device__ uint32_t sup(int k, float4& l, float4& h) const {
@@ -1283,7 +1325,13 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
             if (S.cl_slab) {
               const CullK ck{S.cl_margin, S.cl_margin_lo, S.cull_a, S.cull_b, S.cull_c};
               const f3 dd = mk3(bpermute_f(d.x, cown), bpermute_f(d.y, cown), bpermute_f(d.z, cown));
-              if (cp) cp = cluster_may_pass_slab(clusters.lo_of(c), clusters.hi_of(c), clusters.n_of(c), oo, ii, dd, ck);
+              if (cp) {
+                if (S.cl_obb)
+                  cp = cluster_may_pass_obb(clusters.lo_of(c), clusters.hi_of(c), clusters.n_of(c), clusters.u[c],
+                                            clusters.v[c], clusters.w[c], oo, ii, dd, ck);
+                else
+                  cp = cluster_may_pass_slab(clusters.lo_of(c), clusters.hi_of(c), clusters.n_of(c), oo, ii, dd, ck);
+              }
             } else {
               if (cp) cp = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii, S.cl_margin);
             }

@@ -623,7 +623,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
       else if (MODE == TREE_LDS16S)
         trace_phase<HYBRID, COUNT>(
             S, NodesDerived{s_tree},
-            ClustersSuper{s_tree + S.num_nodes, S.cl_lo, S.cl_hi, S.cl_n}, R, fastAABB,
+            ClustersSuper{s_tree + S.num_nodes, S.cl_lo, S.cl_hi, S.cl_n, S.cl_u, S.cl_v, S.cl_w}, R, fastAABB,
             S.num_materials, cnt, W, P);
       else if (MODE == TREE_PACKED)
         trace_phase<HYBRID, COUNT>(S, NodesPacked{S.pnodes}, ClustersSplit{S.cl_lo, S.cl_hi}, R, fastAABB,
@@ -1974,10 +1974,18 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
       (rc = dupload(c, &de2, ce2.data(), ce2.size())))
     return rc;
   int4* dsp;
-  float4* dn;
-  if ((rc = dupload(c, &dsp, sp.data(), sp.size())) || (rc = dupload(c, &dn, nrm.data(), nrm.size()))) return rc;
+  float4 *dn, *du, *dv, *dw;
+  if ((rc = dupload(c, &dsp, sp.data(), sp.size())) || (rc = dupload(c, &dn, nrm.data(), nrm.size())) ||
+      (rc = dupload(c, &du, cs.obb_u.data(), cs.obb_u.size())) ||
+      (rc = dupload(c, &dv, cs.obb_v.data(), cs.obb_v.size())) ||
+      (rc = dupload(c, &dw, cs.obb_w.data(), cs.obb_w.size())))
+    return rc;
   c->S.cl_n = dn;
   c->S.cl_slab = 1;
+  c->S.cl_u = du;
+  c->S.cl_v = dv;
+  c->S.cl_w = dw;
+  c->S.cl_obb = 1;
   set_cull(c, cluster_margin(cv0, ce1, ce2));
   c->S.sup = dsp;
   // a super box past the half range (+-65504) would be infinite, its centre NaN and the cull wrong: such a
@@ -2583,6 +2591,8 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     if (!(value > 0.0 && value <= 1.0)) return fail(KDPT_ERR_ARG, "trace_grid_frac must be in (0, 1]");
     c->trace_grid = std::max(1, (int)(c->full_trace_grid * value));
     c->grid_env = value < 1.0;
+  } else if (k == "cluster_obb") {
+    c->S.cl_obb = v != 0;
   } else if (k == "tree_format" || k == "tree_global" || k == "super_cull" || k == "cluster_slab") {
     if (k == "tree_format") {
       if (v != 0 && v != 16 && v != 32) return fail(KDPT_ERR_ARG, "tree_format must be 0 (best), 16 or 32");

@@ -30,7 +30,7 @@ const char* kGenName[NGEN] = {"random", "graze", "graze_edge", "face", "axis", "
 struct Counts {
   long long lines = 0, pass = 0;           // lines tested, (line, cluster) pairs with a u/v pass
   long long culled_box = 0, viol_box = 0;  // one-level cull (dragon_5's LDS route)
-  long long viol_slab = 0, viol_super = 0, viol_chunk = 0;
+  long long viol_slab = 0, viol_super = 0, viol_chunk = 0, viol_obb = 0;
   long long nofast = 0;                    // some invdir component infinite: the wave does not cull
   long long margin_used = 0;               // passing pairs the box cull passes only thanks to the margin
   // over the passing (line, triangle) pairs: the largest distance of the line's exact crossing of the
@@ -39,7 +39,7 @@ struct Counts {
   double bound = 0.0;  // the largest distance / error bound over every pass (must be <= 1)
   void add(const Counts& o) {
     lines += o.lines; pass += o.pass; culled_box += o.culled_box; viol_box += o.viol_box;
-    viol_slab += o.viol_slab; viol_super += o.viol_super; viol_chunk += o.viol_chunk;
+    viol_slab += o.viol_slab; viol_super += o.viol_super; viol_chunk += o.viol_chunk; viol_obb += o.viol_obb;
     nofast += o.nofast; margin_used += o.margin_used; worst = std::max(worst, o.worst);
     bound = std::max(bound, o.bound);
   }
@@ -99,8 +99,8 @@ int rays_check(const char* path, const ClusterSet& cs, float K, const CullK& ck)
     const uint32_t w = (uint32_t)cs.sup[s].w;
     for (uint32_t k = 0; k <= (w & 31u); k++) super_of[(w >> 5) + k] = (int)s;
   }
-  long long pairs = 0, culled = 0, viol_box = 0, viol_slab = 0, viol_super = 0, nofast = 0, passes = 0;
-#pragma omp parallel for schedule(dynamic, 256) reduction(+ : pairs, culled, viol_box, viol_slab, viol_super, nofast, passes)
+  long long pairs = 0, culled = 0, viol_box = 0, viol_slab = 0, viol_super = 0, viol_obb = 0, nofast = 0, passes = 0;
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : pairs, culled, viol_box, viol_slab, viol_super, viol_obb, nofast, passes)
   for (long long i = 0; i < nr; i++) {
     const f3 o = mk3(r[6 * i], r[6 * i + 1], r[6 * i + 2]), d = mk3(r[6 * i + 3], r[6 * i + 4], r[6 * i + 5]);
     const f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -113,6 +113,7 @@ int rays_check(const char* path, const ClusterSet& cs, float K, const CullK& ck)
       const float4 L = cs.lo[c], H = cs.hi[c];
       const bool box = cluster_may_pass(L, H, o, inv, K);
       const bool slab = cluster_may_pass_slab(L, H, cs.nrm[c], o, inv, d, ck);
+      const bool obb = cluster_may_pass_obb(L, H, cs.nrm[c], cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ck);
       bool sup = true;
       if (super_of[c] >= 0) {
         const int4 q = cs.sup[super_of[c]];
@@ -120,7 +121,7 @@ int rays_check(const char* path, const ClusterSet& cs, float K, const CullK& ck)
         const float4 sh = make_float4(half_hi((uint32_t)q.y), half_lo((uint32_t)q.z), half_hi((uint32_t)q.z), 0);
         sup = cluster_may_pass(sl, sh, o, inv, K);
       }
-      if (box && slab && sup) continue;
+      if (box && slab && sup && obb) continue;
       culled++;
       const int2 inf = cs.info[c];
       bool pass = false;
@@ -133,12 +134,14 @@ int rays_check(const char* path, const ClusterSet& cs, float K, const CullK& ck)
         viol_box += !box;
         viol_slab += !slab;
         viol_super += !sup;
+        viol_obb += !obb;
       }
     }
   }
   printf("{\"rays\": %lld, \"clusters\": %d, \"margin\": %.9g, \"pairs\": %lld, \"culled\": %lld, \"nofast\": %lld, "
-         "\"viol_box\": %lld, \"viol_slab\": %lld, \"viol_super\": %lld, \"violations\": %lld}\n",
-         nr, ncl, (double)K, pairs, culled, nofast, viol_box, viol_slab, viol_super, viol_box + viol_slab + viol_super);
+         "\"viol_box\": %lld, \"viol_slab\": %lld, \"viol_super\": %lld, \"viol_obb\": %lld, \"violations\": %lld}\n",
+         nr, ncl, (double)K, pairs, culled, nofast, viol_box, viol_slab, viol_super, viol_obb,
+         viol_box + viol_slab + viol_super + viol_obb);
   return 0;
 }
 
@@ -373,6 +376,7 @@ int main(int argc, char** argv) {
         if (!box) C.viol_box++;
         if (box && !cluster_may_pass(L, H, of, inv, 0.0f)) C.margin_used++;
         if (!cluster_may_pass_slab(L, H, cs.nrm[c], of, inv, df, ck)) C.viol_slab++;
+        if (!cluster_may_pass_obb(L, H, cs.nrm[c], cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], of, inv, df, ck)) C.viol_obb++;
         if (super_of[c] >= 0) {
           const int4 q = cs.sup[super_of[c]];
           const float4 sl = make_float4(half_lo((uint32_t)q.x), half_hi((uint32_t)q.x), half_lo((uint32_t)q.y), 0);
@@ -396,12 +400,12 @@ int main(int argc, char** argv) {
     const Counts& C = tot[g];
     all.add(C);
     printf("%s\"%s\": {\"lines\": %lld, \"pass\": %lld, \"culled_box\": %lld, \"viol_box\": %lld, \"viol_slab\": %lld, "
-           "\"viol_super\": %lld, \"viol_chunk\": %lld, \"nofast\": %lld, \"margin_used\": %lld, \"worst\": %.4g, \"bound\": %.4g}",
+           "\"viol_super\": %lld, \"viol_chunk\": %lld, \"viol_obb\": %lld, \"nofast\": %lld, \"margin_used\": %lld, \"worst\": %.4g, \"bound\": %.4g}",
            g ? ", " : "", kGenName[g], C.lines, C.pass, C.culled_box, C.viol_box, C.viol_slab, C.viol_super,
-           C.viol_chunk, C.nofast, C.margin_used, C.worst, C.bound);
+           C.viol_chunk, C.viol_obb, C.nofast, C.margin_used, C.worst, C.bound);
   }
   printf("}, \"violations\": %lld, \"lines\": %lld, \"pass\": %lld, \"margin_used\": %lld, \"worst\": %.4g, \"bound\": %.4g}\n",
-         all.viol_box + all.viol_slab + all.viol_super + all.viol_chunk, all.lines, all.pass, all.margin_used,
+         all.viol_box + all.viol_slab + all.viol_super + all.viol_chunk + all.viol_obb, all.lines, all.pass, all.margin_used,
          all.worst, all.bound);
   return 0;
 }

@@ -40,13 +40,14 @@ HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_traceILb1ELb0ELi
 # The derived-box route (NodesDerived, the C5 icosphere's tree in LDS) keeps the current node's box in 6 more
 # registers at the same 96-VGPR cap; its spills are the price of the tree in LDS (+10.6 % on C5, and a 4-wave
 # cap without spills measured 8 % slower; profiles/r03_ab_log.md)
-# The two-level cull route (TREE_LDS16S, the C5 icosphere) adds the super pass's survivor bookkeeping on top.
+# The two-level cull route (TREE_LDS16S, the C5 icosphere) adds the super pass's survivor bookkeeping on top,
+# and the oriented-box second level (three slabs) 16 B more: measured +3.9 % on C5 all the same (r04_ab_log.md).
 # Batches of up to 16 iterations per intersect launch (MAXB) cost the derived-box routes a few more bytes.
 # TREE_LDS16 (mode 3: derived records with the cluster boxes in LDS, e.g. the level-6 icosphere) measured
 # 60 / 44 B with MAXB 16.
 SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 32, "k_traceILb0ELb0ELi2E": 32, "k_traceILb1ELb0ELi3E": 64,
               "k_traceILb0ELb0ELi3E": 64, "k_traceILb1ELb0ELi4E": 88,
-              "k_traceILb0ELb0ELi4E": 88, "k_traceILb1ELb0ELi5E": 100, "k_traceILb0ELb0ELi5E": 100,
+              "k_traceILb0ELb0ELi4E": 88, "k_traceILb1ELb0ELi5E": 116, "k_traceILb0ELb0ELi5E": 116,
               "k_shade_fused": 20}
 
 

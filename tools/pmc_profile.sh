@@ -15,7 +15,7 @@ export TMPDIR=/tmp
 BENCH=(bench.py --no-cpu-baseline "$@")
 # the fixed step counts come last (argparse: the last one wins), so workload args pass through but the PMC
 # passes always count exactly the dispatches of the one timed step the summariser divides by
-PMC_BENCH=(bench.py --no-cpu-baseline "$@" --steps 1 --warmup 0 --spp-per-step 8)
+PMC_BENCH=(bench.py --no-cpu-baseline "$@" --steps 1 --warmup 0 --spp-per-step 16)
 run() {  # name, then rocprofv3 args; a time-out or crash stops the script
   local name=$1
   shift
