@@ -83,7 +83,7 @@ def main():
                                 "cus": sum(g // wg if wg == 1024 else g // wg for g, wg in e["grid"].values())}
                             for f, e in fam.items()}
     out["bench_under_pmc"] = b
-    iters = b["config"]["spp_per_step"] * b["steps"]
+    iters = b["config"].get("spp_per_frame", b["config"].get("spp_per_step")) * b["steps"]
     rays = b["roofline"]["rays_per_launch"] * b["roofline"]["launches"]  # k_trace rays of the timed iterations
     segs = b["segments_per_iteration"] * (iters + 1)  # shading also ran the counting iteration
     P = out["passes"]
