@@ -235,7 +235,9 @@ int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
  * "shade_batch" (1; 0 = one k_shade_fused launch per iteration instead of one per batch), "gen_geoms" (1;
  * 0 = camera rays and bounce 0's k_geoms as two launches instead of one k_gen_geoms_b),
  * "tree_format" (0 = best fit; 16 / 32 = only that LDS record size), "super_cull" (1; 0 = no two-level
- * super-cluster route), "cluster_slab" (1; 0 = no normal slab in the second cull level),
+ * super-cluster route), "cluster_slab" (1; 0 = no normal slab in the second cull level), "cluster_obb" (1;
+ * 0 = the second level tests the axis-aligned box and the normal slab only, not the oriented box),
+ * "super_slab" (1; 0 = the first level tests the super-clusters' boxes only, not their slabs),
  * "cluster_cull" (1; 0 = no cluster / chunk cull at all: every big-leaf cluster is swept, exact by
  * construction), "cull_margin" (0 = the scene's; > 0 overrides the cull's margin coefficient),
  * "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots (they are remade). */

@@ -56,6 +56,7 @@ constexpr double CULL_RHO_CAP = 64.0;  // |e1| |e2| / |e1 x e2| beyond which a t
 struct ClusterSet {
   std::vector<int2> leaf_cl, leaf_sp;  // per node: {first cluster, count} / {first super, count}
   std::vector<int4> sup;               // super-cluster records (DevScene::sup)
+  std::vector<float4> sup_n, sup_b;    // the supers' slabs (DevScene::sup_n, sup_b)
   std::vector<float4> lo, hi, nrm;     // cluster boxes (w: slab bounds) and slab normals
   std::vector<float4> obb_u, obb_v, obb_w;  // the patch's in-plane slabs (DevScene::cl_u, cl_v, cl_w)
   std::vector<float4> cv0, ce1, ce2;   // cluster-order triangles, CLUSTER per cluster (ce1.w = original index)
@@ -248,6 +249,57 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
         if ((q & 0x7c00u) == 0x7c00u) cs.supers_finite = false;  // beyond the half range: no super route
       cs.sup.push_back(make_int4((int)(lx | ly << 16), (int)(lz | hx << 16), (int)(hy | hz << 16),
                                  (int)((uint32_t)(c0 + b) << 5 | (uint32_t)(cnt - 1))));
+      // the super's own slab (the first cull level's direction-dependent test, DevScene::sup_n / sup_b): the
+      // normalised sum of its triangles' area vectors, the largest chord to their unit normals (4 when a
+      // sliver or a zero sum leaves no bound), and [min, max] of n . (q - c) over the triangles glm tests
+      // (v0, v0 + e1, v0 + e2 exact in double), c the centre the kernel forms from the half-precision box
+      const float cs0[3] = {0.5f * (half_to_float(lx) + half_to_float(hx)), 0.5f * (half_to_float(ly) + half_to_float(hy)),
+                            0.5f * (half_to_float(lz) + half_to_float(hz))};
+      double sn[3] = {0, 0, 0};
+      const int e0 = cs.info[c0 + b].x, e1n = cs.info[c0 + b + cnt - 1].x + cs.info[c0 + b + cnt - 1].y;
+      for (int e = e0; e < e1n; e++) {
+        if (fbits(cs.ce1[e].w) < 0) continue;  // padding
+        const double ax = cs.ce1[e].x, ay = cs.ce1[e].y, az = cs.ce1[e].z;
+        const double bx = cs.ce2[e].x, by = cs.ce2[e].y, bz = cs.ce2[e].z;
+        sn[0] += ay * bz - az * by;
+        sn[1] += az * bx - ax * bz;
+        sn[2] += ax * by - ay * bx;
+      }
+      const double snl = std::sqrt(sn[0] * sn[0] + sn[1] * sn[1] + sn[2] * sn[2]);
+      float nfs[3] = {0.0f, 0.0f, 0.0f};
+      double spread = 4.0, dmn = -1e300, dmx = 1e300;
+      if (snl > 0 && std::isfinite(snl)) {
+        for (int a = 0; a < 3; a++) nfs[a] = (float)(sn[a] / snl);
+        spread = 0.0;
+        dmn = 1e300;
+        dmx = -1e300;
+        for (int e = e0; e < e1n; e++) {
+          if (fbits(cs.ce1[e].w) < 0) continue;
+          const double ax = cs.ce1[e].x, ay = cs.ce1[e].y, az = cs.ce1[e].z;
+          const double bx = cs.ce2[e].x, by = cs.ce2[e].y, bz = cs.ce2[e].z;
+          const double Nx = ay * bz - az * by, Ny = az * bx - ax * bz, Nz = ax * by - ay * bx;
+          const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+          const double E = std::sqrt(ax * ax + ay * ay + az * az) * std::sqrt(bx * bx + by * by + bz * bz);
+          if (Nl == 0.0 || E > CULL_RHO_CAP * Nl) {
+            if (E > 0.3) spread = 4.0;
+          } else if (spread < 4.0) {
+            const double cx = Nx / Nl - nfs[0], cy = Ny / Nl - nfs[1], cz = Nz / Nl - nfs[2];
+            spread = std::max(spread, std::sqrt(cx * cx + cy * cy + cz * cz));
+          }
+          const double v0[3] = {cs.cv0[e].x, cs.cv0[e].y, cs.cv0[e].z};
+          for (int q = 0; q < 3; q++) {
+            const double p[3] = {v0[0] + (q == 1 ? ax : (q == 2 ? bx : 0.0)) - cs0[0],
+                                 v0[1] + (q == 1 ? ay : (q == 2 ? by : 0.0)) - cs0[1],
+                                 v0[2] + (q == 1 ? az : (q == 2 ? bz : 0.0)) - cs0[2]};
+            const double dv = (double)nfs[0] * p[0] + (double)nfs[1] * p[1] + (double)nfs[2] * p[2];
+            dmn = std::min(dmn, dv);
+            dmx = std::max(dmx, dv);
+          }
+        }
+      }
+      cs.sup_n.push_back(make_float4(nfs[0], nfs[1], nfs[2], std::nextafter((float)std::min(spread, 4.0), FLT_MAX)));
+      cs.sup_b.push_back(make_float4(dmn < -1e38 ? -FLT_MAX : std::nextafter((float)dmn, -FLT_MAX),
+                                     dmx > 1e38 ? FLT_MAX : std::nextafter((float)dmx, FLT_MAX), 0.0f, 0.0f));
     }
   }
 }

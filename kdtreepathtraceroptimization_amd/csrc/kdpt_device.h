@@ -120,6 +120,13 @@ struct DevScene {
   // of its first cluster (TREE_LDS16S: records and supers in LDS, the two-level cull), or null
   const int4* sup;
   int num_supers;
+  // per super-cluster: the unit normal of its triangles' summed area vectors and the largest chord to their
+  // unit normals (sup_n = (n, chord)), and the slab [sup_b.x, sup_b.y] of n . (q - c) holding them (c: the
+  // centre of the half-precision box); the first cull level tests survivors of the box against it with the
+  // direction-dependent margin when sup_slab is set (knob "super_slab")
+  const float4* sup_n;
+  const float4* sup_b;
+  int sup_slab;
   // per cluster: the unit normal of its triangles' summed area vectors (xyz); every point q of its triangles
   // has n . (q - c) in [cl_lo.w, cl_hi.w], c = 0.5f * (lo + hi) (bounds rounded outward); n = 0: no slab.
   // The two-level cull tests the line against this slab as well as the box (knob "cluster_slab")
@@ -1301,6 +1308,17 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
           const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
           if (pass) pass = cluster_may_pass(slo, shi, oo, ii, S.cl_margin);
+          // the boxes' survivors against the super's slab (its record from L2), with the margin its normal
+          // spread allows for this direction
+          if (S.sup_slab && __any(pass)) {
+            const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
+            const CullK ck{S.cl_margin, S.cl_margin_lo, S.cull_a, S.cull_b, S.cull_c};
+            if (pass) {
+              const float4 sn = S.sup_n[sp], sb = S.sup_b[sp];
+              pass = cluster_may_pass_slab(make_float4(slo.x, slo.y, slo.z, sb.x), make_float4(shi.x, shi.y, shi.z, sb.y),
+                                           sn, oo, ii, dd, ck);
+            }
+          }
         }
         const unsigned long long sm = __ballot(pass);
         const int nsv = __popcll(sm);

@@ -205,10 +205,9 @@ constexpr int trace_block() { return MODE == 2 ? TRACE_BLOCK : (MODE >= 3 ? TRAC
 #endif
 constexpr int MAXB = KDPT_MAXB;
 struct TraceIter {
-  PathBuf paths;
   const int* cand;      // k_geoms' list of the paths whose ray meets the KD root box (queue slot -> path)
   const int* ccount;    // ... and its length per bounce
-  const int2* geomhit;  // k_geoms' {t_min bits, geom index} per path
+  const float4* cray;   // ... and their rays in queue order: [2 slot] = {origin, t_min}, [2 slot + 1] = {dir, geom}
   int2* hits;
 };
 
@@ -350,18 +349,17 @@ constexpr int GEN_BLOCK = KDPT_GEN_BLOCK;
 // ~100 us at 800x800).  Every thread of the workgroup must call it.
 template <int TB = GEN_BLOCK>
 __device__ __attribute__((always_inline)) inline void geoms_core(const DevScene& S, bool live, int i, f3 o, f3 d,
-                                                                 int2* __restrict__ geomhit, int2* __restrict__ hits,
+                                                                 float4* __restrict__ cray, int2* __restrict__ hits,
                                                                  int* __restrict__ cand, int* __restrict__ ccnt,
                                                                  Counters* count_aabb) {
   const bool kd = S.has_obj && S.num_nodes > 0;
   bool tested = false, walk = false;  // traversed at all / goes on to the intersect kernel
+  float t_min = 0.0f;
+  int hit = -1;
   if (live) {
-    float t_min;
-    int hit;
     tested = kd;
     walk = prep_ray(S, kd, o, d, t_min, hit);
-    if (walk) geomhit[i] = make_int2(fbits(t_min), hit);
-    else hits[i] = make_int2(hit, -1);  // final: the analytic geoms' hit (code -1: none)
+    if (!walk) hits[i] = make_int2(hit, -1);  // final: the analytic geoms' hit (code -1: none)
   }
   __shared__ int s_wcount[TB / 64], s_base;
   const unsigned long long wm = __ballot(walk);
@@ -386,11 +384,16 @@ __device__ __attribute__((always_inline)) inline void geoms_core(const DevScene&
     s_base = tot ? atomicAdd(ccnt, tot) : 0;
   }
   __syncthreads();
-  if (walk) cand[s_base + s_wcount[wv] + (int)lane_prefix(wm)] = i;
+  if (walk) {
+    const int slot = s_base + s_wcount[wv] + (int)lane_prefix(wm);
+    cand[slot] = i;
+    cray[2 * slot] = make_float4(o.x, o.y, o.z, t_min);
+    cray[2 * slot + 1] = make_float4(d.x, d.y, d.z, ibits(hit));
+  }
 }
 
 __device__ __attribute__((always_inline)) inline void geoms_body(const DevScene& S, PathBuf paths, const int* counts,
-                                                                 int depth, int2* __restrict__ geomhit,
+                                                                 int depth, float4* __restrict__ cray,
                                                                  int2* __restrict__ hits, int* __restrict__ cand,
                                                                  int* __restrict__ ccount, Counters* count_aabb,
                                                                  unsigned long long* gspan) {
@@ -406,7 +409,7 @@ __device__ __attribute__((always_inline)) inline void geoms_body(const DevScene&
     o = mk3(q0.x, q0.y, q0.z);
     d = mk3(q1.x, q1.y, q1.z);
   }
-  geoms_core<GEN_BLOCK>(S, live, i, o, d, geomhit, hits, cand, ccount + depth, count_aabb);
+  geoms_core<GEN_BLOCK>(S, live, i, o, d, cray, hits, cand, ccount + depth, count_aabb);
   if (threadIdx.x == 0) atomicMax(&gspan[2 * depth + 1], (unsigned long long)__builtin_amdgcn_s_memrealtime());
 }
 
@@ -414,7 +417,7 @@ __device__ __attribute__((always_inline)) inline void geoms_body(const DevScene&
 struct GeomsIter {
   PathBuf paths;
   const int* counts;
-  int2* geomhit;
+  float4* cray;
   int2* hits;
   int* cand;
   int* ccount;
@@ -428,7 +431,7 @@ struct GeomsBatch {
 };
 __global__ __launch_bounds__(GEN_BLOCK) void k_geoms_b(GeomsBatch B) {
   const GeomsIter& g = B.it[blockIdx.y];
-  geoms_body(B.S, g.paths, g.counts, B.depth, g.geomhit, g.hits, g.cand, g.ccount, B.count_aabb, B.gspan);
+  geoms_body(B.S, g.paths, g.counts, B.depth, g.cray, g.hits, g.cand, g.ccount, B.count_aabb, B.gspan);
 }
 
 // A batch's camera rays and their bounce-0 intersect-stage first part in one launch (blockIdx.y = iteration):
@@ -440,7 +443,7 @@ __global__ __launch_bounds__(GEN_BLOCK) void k_geoms_b(GeomsBatch B) {
 struct GenGeomsIter {
   int* ccount0;       // this use's bounce-0 candidate counter
   int* ccount0_next;  // the next use's (zeroed here)
-  int2* geomhit;
+  float4* cray;
   int2* hits;
   int* cand;
 };
@@ -459,7 +462,7 @@ __global__ __launch_bounds__(GEN_BLOCK) void k_gen_geoms_b(GenGeomsBatch B) {
                                    g.zero_image, o, d);
   const int i = blockIdx.x * blockDim.x + threadIdx.x;
   if (i == 0) *q.ccount0_next = 0;
-  geoms_core<GEN_BLOCK>(B.S, valid && B.g.traceDepth > 0, i, o, d, q.geomhit, q.hits, q.cand, q.ccount0,
+  geoms_core<GEN_BLOCK>(B.S, valid && B.g.traceDepth > 0, i, o, d, q.cray, q.hits, q.cand, q.ccount0,
                         B.count_aabb);
 }
 
@@ -584,24 +587,22 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
 #pragma unroll
         for (int q = 1; q < MAXB; q++) b += k >= pre[q];
         const int* cand = A.it[0].cand;
-        const float4 *p0 = A.it[0].paths.p0, *p1 = A.it[0].paths.p1;
-        const int2* ghp = A.it[0].geomhit;
+        const float4* cray = A.it[0].cray;
         int local = k;
 #pragma unroll
         for (int q = 1; q < MAXB; q++)
           if (b == q) {
             cand = A.it[q].cand;
-            p0 = A.it[q].paths.p0;
-            p1 = A.it[q].paths.p1;
-            ghp = A.it[q].geomhit;
+            cray = A.it[q].cray;
             local = k - pre[q];
           }
+        // the slot's path index and its ray (written in queue order with the slot): three independent loads
+        // of consecutive slots, not a slot load followed by scattered path loads
         const int i = cand[local];
-        const float4 q0 = p0[i], q1 = p1[i];
-        const int2 gh = ghp[i];
+        const float4 q0 = cray[2 * local], q1 = cray[2 * local + 1];
         pidx = i;
         pb = b;
-        wave_ray_start(S, R, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z), u2f((uint32_t)gh.x), gh.y, W);
+        wave_ray_start(S, R, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z), q0.w, fbits(q1.w), W);
       }
     }
     if (COUNT) prof_lap(P, PROF_SETUP_CYC);
@@ -1157,7 +1158,7 @@ struct FuseArgs {
   unsigned long long* lb;     // [cap][ntiles] look-back records
   int* counts;                // [cap + 2] live paths per bounce
   int* ccount;                // [cap] candidates per bounce
-  int2* geomhit;
+  float4* cray;
   int2* hits;
   int* cand;
 };
@@ -1325,8 +1326,10 @@ __device__ __attribute__((always_inline)) inline void shade_tile(const ShadeArgs
     F.dst.pm[d] = o.pm;
     if (A.prep_on) {
       if (o.walk) {
-        F.geomhit[d] = make_int2(fbits(o.tm), o.gh);
-        F.cand[bW + lane_prefix(mw)] = d;
+        const int slot = (int)(bW + lane_prefix(mw));
+        F.cand[slot] = d;
+        F.cray[2 * slot] = make_float4(o.q0.x, o.q0.y, o.q0.z, o.tm);
+        F.cray[2 * slot + 1] = make_float4(o.q1.x, o.q1.y, o.q1.z, ibits(o.gh));
       } else {
         F.hits[d] = make_int2(o.gh, -1);  // final: the analytic geoms' hit (code -1: none)
       }
@@ -1455,7 +1458,7 @@ __global__ __launch_bounds__(SCAN_TB) void k_scan(ScanJob j0, ScanJob j1, const 
 struct ScatterPrep {
   int on;
   const int2* prep;
-  int2* geomhit;
+  float4* cray;
   int2* hits;
   int* cand;
   const int* tile_coff;
@@ -1516,8 +1519,10 @@ __global__ __launch_bounds__(TILE) void k_scatter(PathBuf src, PathBuf dst, cons
       if (w) {
         int before = 0;
         for (int k = 0; k < wid; k++) before += s_walk[k];
-        P.geomhit[dst_i] = make_int2(pr.x, geom);
-        P.cand[P.tile_coff[tile] + before + (int)lane_prefix(m)] = dst_i;
+        const int slot = P.tile_coff[tile] + before + (int)lane_prefix(m);
+        P.cand[slot] = dst_i;
+        P.cray[2 * slot] = make_float4(q0.x, q0.y, q0.z, u2f((uint32_t)pr.x));
+        P.cray[2 * slot + 1] = make_float4(q1.x, q1.y, q1.z, ibits(geom));
       } else {
         P.hits[dst_i] = make_int2(geom, -1);  // final: the analytic geoms' hit (code -1: none)
       }
@@ -1671,7 +1676,7 @@ struct kdpt_ctx {
   int* counts = nullptr;  // [cap + 2] live paths per bounce, [cap + 2] fault flag, then [cap] work counters
   int* work = nullptr;
   int2* hits = nullptr;   // [npix] hit code + objMaterialIdx from the intersect kernel
-  int2* geomhit = nullptr;  // [npix] analytic-geom t_min bits + index (k_geoms -> k_trace)
+  float4* cray = nullptr;   // [2 npix] the candidates' rays in queue order (k_geoms / shading -> k_trace)
   int* cand = nullptr;      // [npix] paths whose ray meets the KD root box (k_geoms -> k_trace)
   int2* prep = nullptr;     // [npix] next bounce's geoms record + walk flag (k_shade -> k_scatter)
   int* tile_ccounts = nullptr;  // [ntiles] walking survivors per tile, and their offsets
@@ -1822,7 +1827,7 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
   if ((rc = dalloc(c, &c->counts, 4 * (size_t)c->cap + 5)) || (rc = dalloc(c, &c->lb, (size_t)c->cap * c->ntiles)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->cand, (size_t)c->npix)) || (rc = dalloc(c, &c->prep, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->tile_ccounts, (size_t)c->ntiles)) || (rc = dalloc(c, &c->tile_coff, (size_t)c->ntiles)) ||
-      (rc = dalloc(c, &c->geomhit, (size_t)c->npix)) ||
+      (rc = dalloc(c, &c->cray, 2 * (size_t)c->npix)) ||
       (rc = dalloc(c, &c->perm, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->tile_kcounts, (size_t)TRACE_KEYS * c->ntiles)) ||
       (rc = dalloc(c, &c->tile_koff, (size_t)TRACE_KEYS * c->ntiles)) ||
@@ -1986,6 +1991,12 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
   c->S.cl_v = dv;
   c->S.cl_w = dw;
   c->S.cl_obb = 1;
+  float4 *dsn, *dsb;
+  if ((rc = dupload(c, &dsn, cs.sup_n.data(), cs.sup_n.size())) || (rc = dupload(c, &dsb, cs.sup_b.data(), cs.sup_b.size())))
+    return rc;
+  c->S.sup_n = dsn;
+  c->S.sup_b = dsb;
+  c->S.sup_slab = 1;
   set_cull(c, cluster_margin(cv0, ce1, ce2));
   c->S.sup = dsp;
   // a super box past the half range (+-65504) would be infinite, its centre NaN and the cull wrong: such a
@@ -2593,6 +2604,8 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     c->grid_env = value < 1.0;
   } else if (k == "cluster_obb") {
     c->S.cl_obb = v != 0;
+  } else if (k == "super_slab") {
+    c->S.sup_slab = v != 0;
   } else if (k == "tree_format" || k == "tree_global" || k == "super_cull" || k == "cluster_slab") {
     if (k == "tree_format") {
       if (v != 0 && v != 16 && v != 32) return fail(KDPT_ERR_ARG, "tree_format must be 0 (best), 16 or 32");
@@ -3234,7 +3247,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       for (int b = 0; b < nb; b++) {
         kdpt_ctx* c = cs[b];
         c->cc0_cur = c->ccount0 + c->gen_parity;
-        gg.it[b] = GenGeomsIter{c->cc0_cur, c->ccount0 + (c->gen_parity ^ 1), c->geomhit, c->hits, c->cand};
+        gg.it[b] = GenGeomsIter{c->cc0_cur, c->ccount0 + (c->gen_parity ^ 1), c->cray, c->hits, c->cand};
         c->gen_parity ^= 1;
       }
       hipLaunchKernelGGL(k_gen_geoms_b, dim3((c0->npix + GEN_BLOCK - 1) / GEN_BLOCK, nb), dim3(GEN_BLOCK), 0, st,
@@ -3255,10 +3268,9 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     t.prof_steps = (c0->parent ? c0->parent : c0)->profile_steps ? 1 : 0;
     for (int b = 0; b < MAXB; b++) {
       kdpt_ctx* c = cs[b < nb ? b : 0];
-      t.it[b].paths = c->buf[c->cur];
       t.it[b].cand = c->cand;
       t.it[b].ccount = (depth == 0 && gen_geoms) ? c->cc0_cur : c->ccount;  // indexed by depth (0 here)
-      t.it[b].geomhit = c->geomhit;
+      t.it[b].cray = c->cray;
       t.it[b].hits = c->hits;
     }
     t.work = c0->work;
@@ -3315,7 +3327,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         gb.gspan = c0->trace_t + 2 * c0->cap;
         for (int b = 0; b < nb; b++) {
           kdpt_ctx* c = cs[b];
-          gb.it[b] = GeomsIter{c->buf[c->cur], c->counts, c->geomhit, c->hits, c->cand, c->ccount};
+          gb.it[b] = GeomsIter{c->buf[c->cur], c->counts, c->cray, c->hits, c->cand, c->ccount};
         }
         hipLaunchKernelGGL(k_geoms_b, dim3((c0->npix + GEN_BLOCK - 1) / GEN_BLOCK, nb), dim3(GEN_BLOCK), 0, st, gb);
         HIP_TRY(hipGetLastError());
@@ -3364,7 +3376,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
       if (compact && !sort && !a.tile_kcounts && !c->no_fuse) {
         // single pass: shading, compaction into the other buffer and the hand-off (k_shade_fused)
         const int nxt = c->cur ^ 1;
-        const FuseArgs f{c->buf[nxt], c->tickets, c->lb, c->counts, c->ccount, c->geomhit, c->hits, c->cand};
+        const FuseArgs f{c->buf[nxt], c->tickets, c->lb, c->counts, c->ccount, c->cray, c->hits, c->cand};
         const bool stage = c->S.num_geoms + c->S.num_boxes <= ORDERED_GEOMS && c->S.num_materials <= STAGE_MATS;
         const bool hyb = c->opt.short_stack || c->brute;
         const int shade_grid = (c->npix + SHADE_TB - 1) / SHADE_TB;
@@ -3398,7 +3410,7 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         hipLaunchKernelGGL(k_scan, dim3(prep_next ? 2 : 1), dim3(SCAN_TB), 0, st, j0, j1, c->counts, depth, c->ntiles);
         HIP_TRY(hipGetLastError());
         const int nxt = c->cur ^ 1;
-        ScatterPrep sp{prep_next ? 1 : 0, c->prep, c->geomhit, c->hits, c->cand, c->tile_coff};
+        ScatterPrep sp{prep_next ? 1 : 0, c->prep, c->cray, c->hits, c->cand, c->tile_coff};
         if (sort)
           hipLaunchKernelGGL(k_scatter<true>, dim3(c->ntiles), dim3(TILE), 0, st, c->buf[c->cur], c->buf[nxt],
                              c->tile_off, c->counts, depth, c->ntiles, compact ? 1 : 0, sp);

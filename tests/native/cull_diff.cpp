@@ -120,6 +120,9 @@ int rays_check(const char* path, const ClusterSet& cs, float K, const CullK& ck)
         const float4 sl = make_float4(half_lo((uint32_t)q.x), half_hi((uint32_t)q.x), half_lo((uint32_t)q.y), 0);
         const float4 sh = make_float4(half_hi((uint32_t)q.y), half_lo((uint32_t)q.z), half_hi((uint32_t)q.z), 0);
         sup = cluster_may_pass(sl, sh, o, inv, K);
+        const float4 sb = cs.sup_b[super_of[c]];
+        sup = sup && cluster_may_pass_slab(make_float4(sl.x, sl.y, sl.z, sb.x), make_float4(sh.x, sh.y, sh.z, sb.y),
+                                           cs.sup_n[super_of[c]], o, inv, d, ck);
       }
       if (box && slab && sup && obb) continue;
       culled++;
@@ -382,6 +385,10 @@ int main(int argc, char** argv) {
           const float4 sl = make_float4(half_lo((uint32_t)q.x), half_hi((uint32_t)q.x), half_lo((uint32_t)q.y), 0);
           const float4 sh = make_float4(half_hi((uint32_t)q.y), half_lo((uint32_t)q.z), half_hi((uint32_t)q.z), 0);
           if (!cluster_may_pass(sl, sh, of, inv, K)) C.viol_super++;
+          const float4 sb = cs.sup_b[super_of[c]];
+          if (!cluster_may_pass_slab(make_float4(sl.x, sl.y, sl.z, sb.x), make_float4(sh.x, sh.y, sh.z, sb.y),
+                                     cs.sup_n[super_of[c]], of, inv, df, ck))
+            C.viol_super++;
         }
       }
       // the brute-force route: the file-order chunk holding the line's triangle

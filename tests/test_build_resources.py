@@ -36,7 +36,9 @@ HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_traceILb1ELb0ELi
 # 4 waves: the few values that no longer fit are spilled once at the start and reloaded once per round (a node
 # phase + a leaf phase), outside the node and leaf loops; measured +2.8 % overall (profiles/r02_ab_log.md)
 # The max-ILP machine scheduler (the runtime's build flags) spills up to 20 B of the fused shading at its
-# 80-VGPR cap; the build with it measured +1.2 % over the default scheduler's spill-free one (profiles/r02_ab_log.md)
+# 80-VGPR cap; the build with it measured +1.2 % over the default scheduler's spill-free one (profiles/r02_ab_log.md).
+# Writing the candidates' rays in queue order (round 4) takes the per-iteration form (knob shade_batch = 0) to 28 B;
+# the batched k_shade_fused_b the pipeline runs stays at 12 B.
 # The derived-box route (NodesDerived, the C5 icosphere's tree in LDS) keeps the current node's box in 6 more
 # registers at the same 96-VGPR cap; its spills are the price of the tree in LDS (+10.6 % on C5, and a 4-wave
 # cap without spills measured 8 % slower; profiles/r03_ab_log.md)
@@ -48,7 +50,7 @@ HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_traceILb1ELb0ELi
 SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 32, "k_traceILb0ELb0ELi2E": 32, "k_traceILb1ELb0ELi3E": 64,
               "k_traceILb0ELb0ELi3E": 64, "k_traceILb1ELb0ELi4E": 88,
               "k_traceILb0ELb0ELi4E": 88, "k_traceILb1ELb0ELi5E": 116, "k_traceILb0ELb0ELi5E": 116,
-              "k_shade_fused": 20}
+              "k_shade_fused": 28}
 
 
 @pytest.mark.parametrize("frag", sorted(HOT))
