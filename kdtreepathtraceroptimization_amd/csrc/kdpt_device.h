@@ -1301,8 +1301,14 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         const int own = pair_owner(W->slot, excl, nsp, B, carry);
         const int sp = W->tbase[own] + B + lane;
         bool pass = B + lane < P;
-        float4 slo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), shi = slo;
+        float4 slo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), shi = slo, sn = slo, sb = slo;
         uint32_t sinfo = 0u;
+        // the super's slab record (L2) is requested for every pair before the box test, so its latency
+        // overlaps the LDS record, the ray exchange and the box test
+        if (fastAABB && S.sup_slab && pass) {
+          sn = S.sup_n[sp];
+          sb = S.sup_b[sp];
+        }
         if (pass) sinfo = clusters.sup(sp, slo, shi);
         if (fastAABB) {
           const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
@@ -1314,7 +1320,6 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
             const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
             const CullK ck{S.cl_margin, S.cl_margin_lo, S.cull_a, S.cull_b, S.cull_c};
             if (pass) {
-              const float4 sn = S.sup_n[sp], sb = S.sup_b[sp];
               pass = cluster_may_pass_slab(make_float4(slo.x, slo.y, slo.z, sb.x), make_float4(shi.x, shi.y, shi.z, sb.y),
                                            sn, oo, ii, dd, ck);
             }
@@ -1337,6 +1342,17 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
           }
           if (COUNT) prof_add(WP, PROF_BIG_CLUSTERS, (unsigned long long)__popcll(__ballot(cp)));
           if (fastAABB) {
+            // the oriented-box records (L2) requested before the ray exchange, so their latency overlaps it
+            const float4 z4 = make_float4(0.0f, 0.0f, 0.0f, 0.0f);
+            float4 rlo = z4, rhi = z4, rn = z4, ru = z4, rv = z4, rw = z4;
+            if (S.cl_slab && S.cl_obb && cp) {
+              rlo = clusters.lo_of(c);
+              rhi = clusters.hi_of(c);
+              rn = clusters.n_of(c);
+              ru = clusters.u[c];
+              rv = clusters.v[c];
+              rw = clusters.w[c];
+            }
             const f3 oo = mk3(bpermute_f(o.x, cown), bpermute_f(o.y, cown), bpermute_f(o.z, cown));
             const f3 ii =
                 mk3(bpermute_f(invdir.x, cown), bpermute_f(invdir.y, cown), bpermute_f(invdir.z, cown));
@@ -1345,8 +1361,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
               const f3 dd = mk3(bpermute_f(d.x, cown), bpermute_f(d.y, cown), bpermute_f(d.z, cown));
               if (cp) {
                 if (S.cl_obb)
-                  cp = cluster_may_pass_obb(clusters.lo_of(c), clusters.hi_of(c), clusters.n_of(c), clusters.u[c],
-                                            clusters.v[c], clusters.w[c], oo, ii, dd, ck);
+                  cp = cluster_may_pass_obb(rlo, rhi, rn, ru, rv, rw, oo, ii, dd, ck);
                 else
                   cp = cluster_may_pass_slab(clusters.lo_of(c), clusters.hi_of(c), clusters.n_of(c), oo, ii, dd, ck);
               }
