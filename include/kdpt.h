@@ -238,6 +238,8 @@ int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
  * super-cluster route), "cluster_slab" (1; 0 = no normal slab in the second cull level), "cluster_obb" (1;
  * 0 = the second level tests the axis-aligned box and the normal slab only, not the oriented box),
  * "super_slab" (1; 0 = the first level tests the super-clusters' boxes only, not their slabs),
+ * "flat_obb" (1; 0 = the one-level cluster cull tests the clusters' axis-aligned boxes only, not also
+ * their oriented boxes),
  * "cluster_cull" (1; 0 = no cluster / chunk cull at all: every big-leaf cluster is swept, exact by
  * construction), "cull_margin" (0 = the scene's; > 0 overrides the cull's margin coefficient),
  * "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots (they are remade). */

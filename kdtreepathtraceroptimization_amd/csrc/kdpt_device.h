@@ -140,6 +140,9 @@ struct DevScene {
   const float4* cl_v;
   const float4* cl_w;
   int cl_obb;
+  // the one-level route (TREE_LDS / LDS16 / LDS16G...) also tests its box survivors against the cluster's
+  // oriented box from HBM (knob "flat_obb")
+  int flat_obb;
   // the cull's margin coefficients (kdpt_clusters.h cluster_margin): cl_margin for the box-only tests;
   // the slab level uses cull_margin_dir(): max(cl_margin_lo, min(cl_margin, cull_a / g + cull_c)),
   // g = |n . d| - cl_n.w - cull_b
@@ -441,7 +444,10 @@ constexpr int SUPER = KDPT_SUPER;  // clusters per super-cluster
 #ifndef KDPT_BIG_LEAF
 #define KDPT_BIG_LEAF 64  // tools/build_variant.sh experiments only
 #endif
-constexpr int BIG_LEAF = KDPT_BIG_LEAF;  // leaves this size or larger are tested cluster by cluster
+constexpr int BIG_LEAF = KDPT_BIG_LEAF;
+#ifndef KDPT_SMALL_PF
+#define KDPT_SMALL_PF 1  // rounds of small-leaf triangles loaded ahead (tools/build_variant.sh experiments: 2)
+#endif  // leaves this size or larger are tested cluster by cluster
 
 // IEEE half bits -> float (exact).  The device converts in one instruction; g++ 11 has no _Float16.
 KDPT_HD float half_to_float(uint32_t h) {
@@ -1396,7 +1402,19 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         if (fastAABB) {
           const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
-          if (pass) pass = cluster_may_pass(clusters.lo_of(c), clusters.hi_of(c), oo, ii, S.cl_margin);
+          float4 clo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), chi = clo;
+          if (pass) {
+            clo = clusters.lo_of(c);
+            chi = clusters.hi_of(c);
+            pass = cluster_may_pass(clo, chi, oo, ii, S.cl_margin);
+          }
+          // the box's survivors against the cluster's oriented box (its slabs from L2), with the margin of
+          // the second level
+          if (S.flat_obb && __any(pass)) {
+            const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
+            const CullK ck{S.cl_margin, S.cl_margin_lo, S.cull_a, S.cull_b, S.cull_c};
+            if (pass) pass = cluster_may_pass_obb(clo, chi, S.cl_n[c], S.cl_u[c], S.cl_v[c], S.cl_w[c], oo, ii, dd, ck);
+          }
         }
         if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
         sweep(pass, c, own);
@@ -1431,20 +1449,41 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       prof_add(WP, PROF_SMALL_PAIRS, (unsigned long long)P);
     }
     // the next round's owners are found and its triangles loaded while the current round is tested
+    // (SMALL_PF == 2: the next two rounds')
     int carry = 0;
     int owner = pair_owner(W->slot, excl, sz, 0, carry);
     int tri = W->tbase[owner] + lane;
     TriData nxt{};
     if (lane < P) nxt = tri_load(S, tri);
+#if KDPT_SMALL_PF == 2
+    int owner2 = 0, tri2 = 0;
+    TriData nxt2{};
+    if (64 < P) {
+      owner2 = pair_owner(W->slot, excl, sz, 64, carry);
+      tri2 = W->tbase[owner2] + 64 + lane;
+      if (64 + lane < P) nxt2 = tri_load(S, tri2);
+    }
+#endif
     for (int B = 0; B < P; B += 64) {
       const TriData cur_t = nxt;
       const int cowner = owner, ctri = tri;
       const bool valid = B + lane < P;
+#if KDPT_SMALL_PF == 2
+      nxt = nxt2;
+      owner = owner2;
+      tri = tri2;
+      if (B + 128 < P) {
+        owner2 = pair_owner(W->slot, excl, sz, B + 128, carry);
+        tri2 = W->tbase[owner2] + B + 128 + lane;
+        if (B + 128 + lane < P) nxt2 = tri_load(S, tri2);
+      }
+#else
       if (B + 64 < P) {
         owner = pair_owner(W->slot, excl, sz, B + 64, carry);
         tri = W->tbase[owner] + B + 64 + lane;
         if (B + 64 + lane < P) nxt = tri_load(S, tri);
       }
+#endif
       if (valid) {
         const float4 q0 = W->od[cowner];
         const float2 q1 = W->dd[cowner];

@@ -1991,6 +1991,7 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
   c->S.cl_v = dv;
   c->S.cl_w = dw;
   c->S.cl_obb = 1;
+  c->S.flat_obb = 1;
   float4 *dsn, *dsb;
   if ((rc = dupload(c, &dsn, cs.sup_n.data(), cs.sup_n.size())) || (rc = dupload(c, &dsb, cs.sup_b.data(), cs.sup_b.size())))
     return rc;
@@ -2604,6 +2605,8 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     c->grid_env = value < 1.0;
   } else if (k == "cluster_obb") {
     c->S.cl_obb = v != 0;
+  } else if (k == "flat_obb") {
+    c->S.flat_obb = v != 0;
   } else if (k == "super_slab") {
     c->S.sup_slab = v != 0;
   } else if (k == "tree_format" || k == "tree_global" || k == "super_cull" || k == "cluster_slab") {

@@ -319,7 +319,7 @@ def test_tuning_knobs_keep_parity(kdpt):
     for name, val in (("tree_global", 1), ("tree_format", 32), ("tree_format", 16), ("early_walk", 0), ("early_leaf", 65), ("chunk_width0", 64),
                       ("chunk_width1", 8), ("trace_grid_frac", 0.1), ("shade_fused", 0), ("shade_batch", 0),
                       ("gen_geoms", 0), ("cluster_cull", 0), ("cull_margin", 1e-3), ("cluster_obb", 0),
-                      ("super_slab", 0)):
+                      ("super_slab", 0), ("flat_obb", 0)):
         with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
             pt.set_tuning(name, val)
             pt.trace_iterations(1, 8, pipeline=2, batch=4)
