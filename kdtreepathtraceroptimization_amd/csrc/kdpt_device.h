@@ -442,7 +442,7 @@ static_assert(CLUSTER == 64 || CLUSTER == 32, "cluster size");
 #endif
 constexpr int SUPER = KDPT_SUPER;  // clusters per super-cluster
 #ifndef KDPT_BIG_LEAF
-#define KDPT_BIG_LEAF 64  // tools/build_variant.sh experiments only
+#define KDPT_BIG_LEAF 48  // tools/build_variant.sh experiments only
 #endif
 constexpr int BIG_LEAF = KDPT_BIG_LEAF;
 #ifndef KDPT_SMALL_PF
