@@ -1812,18 +1812,21 @@ int segments_from_counts(kdpt_ctx* c) {
 
 // Per-iteration device state: two path buffers, hit records, trace order, tile counts/offsets,
 // live counts + fault word + work counters.  (The scene, image and counters live elsewhere.)
+// The zero fills go on the context's own stream and are waited for: every kernel of the context runs on a
+// non-blocking stream, which does not order itself after the null stream, so a plain hipMemset there could
+// land after the first iteration's camera-ray kernel had set its path count (that iteration would vanish).
 int alloc_iteration_buffers(kdpt_ctx* c) {
   int rc;
   for (int b = 0; b < 2; b++) {
     if ((rc = dalloc(c, &c->buf[b].p0, c->npix)) || (rc = dalloc(c, &c->buf[b].p1, c->npix)) ||
         (rc = dalloc(c, &c->buf[b].p2, c->npix)) || (rc = dalloc(c, &c->buf[b].pm, c->npix)))
       return rc;
-    HIP_TRY(hipMemset(c->buf[b].pm, 0, sizeof(int) * c->npix));
+    HIP_TRY(hipMemsetAsync(c->buf[b].pm, 0, sizeof(int) * c->npix, c->stream));
   }
   // counts[0..cap+1]: live paths per bounce (rewritten every iteration); counts[cap+2]: fault flag;
   // counts[cap+3 ..]: work counters of the persistent intersect kernel
   if ((rc = dalloc(c, &c->trace_t, 4 * (size_t)c->cap))) return rc;
-  HIP_TRY(hipMemset(c->trace_t, 0, sizeof(unsigned long long) * 4 * c->cap));
+  HIP_TRY(hipMemsetAsync(c->trace_t, 0, sizeof(unsigned long long) * 4 * c->cap, c->stream));
   if ((rc = dalloc(c, &c->counts, 4 * (size_t)c->cap + 5)) || (rc = dalloc(c, &c->lb, (size_t)c->cap * c->ntiles)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->cand, (size_t)c->npix)) || (rc = dalloc(c, &c->prep, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->tile_ccounts, (size_t)c->ntiles)) || (rc = dalloc(c, &c->tile_coff, (size_t)c->ntiles)) ||
@@ -1836,8 +1839,9 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
     return rc;
   if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 3), hipHostMallocDefault) != hipSuccess)
     return fail(KDPT_ERR_HIP, "hipHostMalloc");
-  HIP_TRY(hipMemset(c->counts, 0, sizeof(int) * (4 * c->cap + 5)));
-  HIP_TRY(hipMemset(c->lb, 0, sizeof(unsigned long long) * c->cap * c->ntiles));
+  HIP_TRY(hipMemsetAsync(c->counts, 0, sizeof(int) * (4 * c->cap + 5), c->stream));
+  HIP_TRY(hipMemsetAsync(c->lb, 0, sizeof(unsigned long long) * c->cap * c->ntiles, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
   c->S.fault = c->counts + c->cap + 2;
   c->work = c->counts + c->cap + 3;
   c->ccount = c->work + c->cap;
@@ -2168,7 +2172,8 @@ int setup_trace(kdpt_ctx* c) {
 // A ray that needs more node steps than any valid tree allows sets the fault word and stops;
 // the iteration then reports an error instead of returning a silently wrong image.
 int fault_error(kdpt_ctx* c, int code) {
-  (void)hipMemset(c->counts + c->cap + 2, 0, sizeof(int));
+  (void)hipMemsetAsync(c->counts + c->cap + 2, 0, sizeof(int), c->stream);
+  (void)hipStreamSynchronize(c->stream);
   if (code & 32)
     return fail(KDPT_ERR_HIP, "shading: a path's survival differed from its hit record's prediction, code " +
                                   std::to_string(code));
@@ -2533,6 +2538,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   if ((rc = setup_trace(c))) return bail(rc);
   c->S.trip_limit = 8 * std::max(c->S.num_nodes, 1) + 64;
   if ((rc = alloc_iteration_events(c))) return bail(rc);
+  // the scene's uploads (hipMemcpy) complete before any kernel of the context's non-blocking streams
+  HIP_TRY(hipDeviceSynchronize());
   if ((rc = kdpt_reset(c))) return bail(rc);
   *out = c;
   return KDPT_OK;
@@ -2987,7 +2994,7 @@ int kdpt_debug_paths(kdpt_ctx* c, int iter, int stop_depth, kdpt_path_segment* o
   float* saved = c->image;
   float* scratch = nullptr;
   HIP_TRY(hipMalloc((void**)&scratch, sizeof(float) * 3 * (size_t)c->npix));
-  HIP_TRY(hipMemset(scratch, 0, sizeof(float) * 3 * (size_t)c->npix));
+  HIP_TRY(hipMemsetAsync(scratch, 0, sizeof(float) * 3 * (size_t)c->npix, c->stream));
   c->image = scratch;
   unsigned long long* saved_tot = c->total_segments;
   c->total_segments = reinterpret_cast<unsigned long long*>(c->counters);  // scratch word
@@ -3019,8 +3026,8 @@ int kdpt_count_iteration(kdpt_ctx* c, int iter, unsigned long long* aabb_tri_hit
   float* saved = c->image;
   float* scratch = nullptr;
   HIP_TRY(hipMalloc((void**)&scratch, sizeof(float) * 3 * (size_t)c->npix));
-  HIP_TRY(hipMemset(scratch, 0, sizeof(float) * 3 * (size_t)c->npix));
-  HIP_TRY(hipMemset(c->counters, 0, sizeof(Counters)));
+  HIP_TRY(hipMemsetAsync(scratch, 0, sizeof(float) * 3 * (size_t)c->npix, c->stream));
+  HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(Counters), c->stream));
   c->image = scratch;
   unsigned long long* saved_tot = c->total_segments;
   unsigned long long* scratch_tot = nullptr;
