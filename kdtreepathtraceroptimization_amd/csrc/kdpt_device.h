@@ -444,10 +444,10 @@ constexpr int SUPER = KDPT_SUPER;  // clusters per super-cluster
 #ifndef KDPT_BIG_LEAF
 #define KDPT_BIG_LEAF 48  // tools/build_variant.sh experiments only
 #endif
-constexpr int BIG_LEAF = KDPT_BIG_LEAF;
+constexpr int BIG_LEAF = KDPT_BIG_LEAF;  // leaves this size or larger are tested cluster by cluster
 #ifndef KDPT_SMALL_PF
 #define KDPT_SMALL_PF 1  // rounds of small-leaf triangles loaded ahead (tools/build_variant.sh experiments: 2)
-#endif  // leaves this size or larger are tested cluster by cluster
+#endif
 
 // IEEE half bits -> float (exact).  The device converts in one instruction; g++ 11 has no _Float16.
 KDPT_HD float half_to_float(uint32_t h) {
