@@ -189,7 +189,7 @@ int kdpt_create(const kdpt_scene *scene, const kdpt_options *opt, int device, kd
 /* pathtrace(pbo, frame, iter, ...): one iteration (1 sample per pixel); iter is 1-based and
  * seeds the RNG.  Synchronous on return, like the reference. */
 int kdpt_trace_iteration(kdpt_ctx *ctx, int frame, int iter);
-/* Iterations first_iter + k*stride (k < count), in batches of `batch` (<= 8) that share each bounce's
+/* Iterations first_iter + k*stride (k < count), in batches of `batch` (<= 16) that share each bounce's
  * intersect launch, with `pipeline` batches in flight at once (each on its own stream and buffers).
  * Partial images are added into the image in iteration order, so the result is bit-identical to
  * calling kdpt_trace_iteration for each.  Returns after enqueueing; follow with kdpt_synchronize.
