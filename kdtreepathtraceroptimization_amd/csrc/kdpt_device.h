@@ -445,9 +445,6 @@ constexpr int SUPER = KDPT_SUPER;  // clusters per super-cluster
 #define KDPT_BIG_LEAF 48  // tools/build_variant.sh experiments only
 #endif
 constexpr int BIG_LEAF = KDPT_BIG_LEAF;  // leaves this size or larger are tested cluster by cluster
-#ifndef KDPT_SMALL_PF
-#define KDPT_SMALL_PF 1  // rounds of small-leaf triangles loaded ahead (tools/build_variant.sh experiments: 2)
-#endif
 
 // IEEE half bits -> float (exact).  The device converts in one instruction; g++ 11 has no _Float16.
 KDPT_HD float half_to_float(uint32_t h) {
@@ -1448,42 +1445,22 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       prof_add(WP, PROF_SMALL_ROUNDS, (unsigned long long)((P + 63) / 64));
       prof_add(WP, PROF_SMALL_PAIRS, (unsigned long long)P);
     }
-    // the next round's owners are found and its triangles loaded while the current round is tested
-    // (SMALL_PF == 2: the next two rounds')
+    // the next round's owners are found and its triangles loaded while the current round is tested (two
+    // rounds ahead spilled: -8 %, profiles/r04_ab_log.md)
     int carry = 0;
     int owner = pair_owner(W->slot, excl, sz, 0, carry);
     int tri = W->tbase[owner] + lane;
     TriData nxt{};
     if (lane < P) nxt = tri_load(S, tri);
-#if KDPT_SMALL_PF == 2
-    int owner2 = 0, tri2 = 0;
-    TriData nxt2{};
-    if (64 < P) {
-      owner2 = pair_owner(W->slot, excl, sz, 64, carry);
-      tri2 = W->tbase[owner2] + 64 + lane;
-      if (64 + lane < P) nxt2 = tri_load(S, tri2);
-    }
-#endif
     for (int B = 0; B < P; B += 64) {
       const TriData cur_t = nxt;
       const int cowner = owner, ctri = tri;
       const bool valid = B + lane < P;
-#if KDPT_SMALL_PF == 2
-      nxt = nxt2;
-      owner = owner2;
-      tri = tri2;
-      if (B + 128 < P) {
-        owner2 = pair_owner(W->slot, excl, sz, B + 128, carry);
-        tri2 = W->tbase[owner2] + B + 128 + lane;
-        if (B + 128 + lane < P) nxt2 = tri_load(S, tri2);
-      }
-#else
       if (B + 64 < P) {
         owner = pair_owner(W->slot, excl, sz, B + 64, carry);
         tri = W->tbase[owner] + B + 64 + lane;
         if (B + 64 + lane < P) nxt = tri_load(S, tri);
       }
-#endif
       if (valid) {
         const float4 q0 = W->od[cowner];
         const float2 q1 = W->dd[cowner];
