@@ -274,15 +274,21 @@ def main():
     rays = st1.total_trace_rays - st0.total_trace_rays  # handed to k_trace
     kernel_ms = st1.intersect_device_ms_total - st0.intersect_device_ms_total  # device clock, per launch
     launches = st1.intersect_device_launches_total - st0.intersect_device_launches_total
+    # the same launches timed by the HIP events the library records around each one on its own stream
+    # (testing_mode): dispatch to end, as rocprofv3's kernel trace times them
+    ev_ms = st1.intersect_ms_total - st0.intersect_ms_total
+    ev_n = st1.intersect_launches_total - st0.intersect_launches_total
     if dist:
         dev = f"cuda:{local}" if args.dist_backend == "nccl" else "cpu"
-        t = torch.tensor([dt, float(seg), float(rays), kernel_ms, float(launches)], dtype=torch.float64, device=dev)
+        t = torch.tensor([dt, float(seg), float(rays), kernel_ms, float(launches), ev_ms, float(ev_n)],
+                         dtype=torch.float64, device=dev)
         tmax = t[0:1].clone()
         dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
         tsum = t[1:].clone()
         dist.all_reduce(tsum, op=dist.ReduceOp.SUM)
         dt = float(tmax[0])
         seg, rays, kernel_ms, launches = int(tsum[0]), int(tsum[1]), float(tsum[2]), int(tsum[3])
+        ev_ms, ev_n = float(tsum[4]), int(tsum[5])
     if rank == 0 and args.dump_image:
         import numpy as np
         np.save(args.dump_image, image.numpy() if gloo else pt.image().reshape(-1))
@@ -300,6 +306,7 @@ def main():
     alg_bytes = 76 * cand + 52 * (aabb - aabb_prep) + 36 * tri + 40 * hit  # SURVEY 8(d) model, k_trace's part
     roof.update({
         "launch_grid_share": round(share, 4), "avg_launch_ms": round(avg_launch_ms, 5), "launches": launches,
+        "avg_launch_ms_hip_events": round(ev_ms / ev_n, 5) if ev_n else None,
         "rays_per_launch": round(rays_per_launch, 1),
         "k_trace_ms_per_step": round(kernel_ms / max(1, args.steps * world), 4),
         "k_trace_busy_share": round(kernel_ms * share / (dt * 1e3 * world), 4),
