@@ -9,6 +9,7 @@
 #pragma once
 
 #include <algorithm>
+#include <array>
 #include <cfloat>
 #include <cmath>
 #include <utility>
@@ -59,17 +60,119 @@ struct ClusterSet {
   std::vector<float4> sup_n, sup_b;    // the supers' slabs (DevScene::sup_n, sup_b)
   std::vector<float4> lo, hi, nrm;     // cluster boxes (w: slab bounds) and slab normals
   std::vector<float4> obb_u, obb_v, obb_w;  // the patch's in-plane slabs (DevScene::cl_u, cl_v, cl_w)
+  std::vector<float4> kc;              // per cluster: the exact cull's {chord_eff, a, K_rig, c} (cull_k_exact)
   std::vector<float4> cv0, ce1, ce2;   // cluster-order triangles, CLUSTER per cluster (ce1.w = original index)
   std::vector<int2> info;              // {first entry in cv0, triangle count}
   bool supers_finite = true;           // every super box is finite in half precision
 };
 
+// How a big leaf's triangles are grouped into clusters (only the order in which a wave tests them changes).
+struct ClusterGrouping {
+  int mode = 0;         // 0: Morton runs of CLUSTER; 1: normal cones first, then balanced Morton runs per cone
+  double chord = 0.5;   // mode 1: a cone is split while the chord of its unit normals about its axis exceeds this
+  int min_split = 8;    // ... and it holds more than this many triangles
+};
+
+constexpr double ULP_HALF = 5.9604644775390625e-8;  // u = 2^-24
+
+// The exact cull's coefficients of one cluster (ClusterSet::kc, read by cull_k_exact), from the triangles glm
+// tests (v0, e1, e2 as floats; products exact in double):
+//   chord = max |N_t / |N_t| - n| over the triangles with N_t = e1 x e2 != 0 (n: the slab normal nf, as
+//     stored); 4 -- never a usable bound -- when n = 0, or when an exactly degenerate triangle (N_t = 0) has
+//     |e1||e2| > 0.3 (its float determinant can then reach FLT_EPSILON for any direction; below that
+//     |a_t| <= 5.8 u |e1||e2| < FLT_EPSILON and it never passes);
+//   rho = max(1, |e1||e2| / |N_t|) over the same triangles (slivers included: they only raise it);
+//   chord_eff = chord (1 + 8u) + 5.8 u rho (1 + 1e-3) + 32 u, rounded up;
+//   a = 17.5 u rho (1 + 1e-5); K_rig = 8.75 E + c; c = 64 u (1 + max|coord| + max|e|), E = max |e1||e2|
+//   ("Cluster cull": the u/v error bound 17.34 u |s| |e1||e2| / a_t + 2.1 u max|e|).
+inline float4 exact_cull_coef(const float4* e1, const float4* e2, const float4* v0, int n, bool has_n, const float* nf) {
+  const double u = ULP_HALF;
+  double chord = has_n ? 0.0 : 4.0, rho = 1.0, E = 0.0, emax = 0.0, cmax = 0.0;
+  for (int k = 0; k < n; k++) {
+    const double ax = e1[k].x, ay = e1[k].y, az = e1[k].z, bx = e2[k].x, by = e2[k].y, bz = e2[k].z;
+    const double la = std::sqrt(ax * ax + ay * ay + az * az), lb = std::sqrt(bx * bx + by * by + bz * bz);
+    const double Nx = ay * bz - az * by, Ny = az * bx - ax * bz, Nz = ax * by - ay * bx;
+    const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+    E = std::max(E, la * lb);
+    emax = std::max(emax, std::max(la, lb));
+    cmax = std::max(cmax, std::max(std::fabs((double)v0[k].x), std::max(std::fabs((double)v0[k].y),
+                                                                       std::fabs((double)v0[k].z))) + la + lb);
+    if (Nl == 0.0) {
+      if (la * lb > 0.3) chord = 4.0;
+      continue;
+    }
+    rho = std::max(rho, la * lb / Nl);
+    if (has_n) {
+      const double cx = Nx / Nl - nf[0], cy = Ny / Nl - nf[1], cz = Nz / Nl - nf[2];
+      chord = std::max(chord, std::sqrt(cx * cx + cy * cy + cz * cz));
+    }
+  }
+  const double c = 64.0 * u * (1.0 + cmax + emax);
+  const double ce = chord >= 2.0 ? 4.0 : chord * (1.0 + 8.0 * u) + 5.8 * u * rho * (1.0 + 1e-3) + 32.0 * u;
+  auto up = [](double x) { return std::nextafter((float)x, FLT_MAX); };
+  return make_float4(up(ce), up(17.5 * u * rho * (1.0 + 1e-5)), up(8.75 * E + c), up(c));
+}
+
+// Mode 1's cones: recursive median splits of the leaf's triangles along the principal axis of their unit
+// normals (power iteration on the 3 x 3 second-moment matrix, in double; deterministic), until each cone's
+// chord max |N_t / |N_t| - n| (n: the normalised sum of its area vectors, as the cluster slab forms it) is at
+// most g.chord.  Exactly degenerate triangles (N_t = 0) have no normal and do not count towards a chord.
+inline void normal_cones(const std::vector<std::array<double, 3>>& A, std::vector<int>& idx, int b, int e,
+                         const ClusterGrouping& g, std::vector<std::pair<int, int>>& out) {
+  double m[3] = {0, 0, 0};
+  for (int k = b; k < e; k++)
+    for (int a = 0; a < 3; a++) m[a] += A[idx[k]][a];
+  const double ml = std::sqrt(m[0] * m[0] + m[1] * m[1] + m[2] * m[2]);
+  double chord = ml > 0 ? 0.0 : 4.0;
+  std::vector<std::array<double, 3>> un(e - b);
+  for (int k = b; k < e; k++) {
+    const std::array<double, 3>& q = A[idx[k]];
+    const double l = std::sqrt(q[0] * q[0] + q[1] * q[1] + q[2] * q[2]);
+    un[k - b] = l > 0 ? std::array<double, 3>{q[0] / l, q[1] / l, q[2] / l} : std::array<double, 3>{0, 0, 0};
+    if (l > 0 && ml > 0) {
+      const double cx = un[k - b][0] - m[0] / ml, cy = un[k - b][1] - m[1] / ml, cz = un[k - b][2] - m[2] / ml;
+      chord = std::max(chord, std::sqrt(cx * cx + cy * cy + cz * cz));
+    }
+  }
+  if (chord <= g.chord || e - b <= g.min_split) {
+    out.push_back({b, e});
+    return;
+  }
+  double M[3][3] = {{0, 0, 0}, {0, 0, 0}, {0, 0, 0}}, mu[3] = {0, 0, 0};
+  for (const auto& q : un)
+    for (int a = 0; a < 3; a++) mu[a] += q[a] / (e - b);
+  for (const auto& q : un)
+    for (int a = 0; a < 3; a++)
+      for (int c = 0; c < 3; c++) M[a][c] += (q[a] - mu[a]) * (q[c] - mu[c]);
+  int a0 = 0;
+  for (int a = 1; a < 3; a++)
+    if (M[a][a] > M[a0][a0]) a0 = a;
+  double p[3] = {a0 == 0 ? 1.0 : 0.0, a0 == 1 ? 1.0 : 0.0, a0 == 2 ? 1.0 : 0.0};
+  for (int it = 0; it < 32; it++) {
+    double r[3];
+    for (int a = 0; a < 3; a++) r[a] = M[a][0] * p[0] + M[a][1] * p[1] + M[a][2] * p[2];
+    const double rl = std::sqrt(r[0] * r[0] + r[1] * r[1] + r[2] * r[2]);
+    if (!(rl > 0)) break;
+    for (int a = 0; a < 3; a++) p[a] = r[a] / rl;
+  }
+  std::vector<std::pair<double, int>> key(e - b);
+  for (int k = b; k < e; k++) key[k - b] = {p[0] * un[k - b][0] + p[1] * un[k - b][1] + p[2] * un[k - b][2], idx[k]};
+  std::stable_sort(key.begin(), key.end(),
+                   [](const std::pair<double, int>& x, const std::pair<double, int>& y) { return x.first < y.first; });
+  for (int k = b; k < e; k++) idx[k] = key[k - b].second;
+  const int mid = b + (e - b) / 2;
+  normal_cones(A, idx, b, mid, g, out);
+  normal_cones(A, idx, mid, e, g, out);
+}
+
 // Big leaves as clusters of <= CLUSTER triangles: Morton order of the triangle centroids inside the leaf's
-// box, consecutive runs of CLUSTER, each with its exact float box, the slab along its summed area vector, and runs of
-// SUPER clusters under one half-precision box rounded outward.
+// box (mode 1: within each normal cone), consecutive runs, each with its exact float box, the slab along its
+// summed area vector, its oriented box and its exact-cull coefficients, and runs of SUPER clusters under one
+// half-precision box rounded outward.
 inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tri_bare* tris,
                               const std::vector<float4>& tv, const std::vector<float4>& e1,
-                              const std::vector<float4>& e2, ClusterSet& cs) {
+                              const std::vector<float4>& e2, ClusterSet& cs,
+                              const ClusterGrouping& grouping = ClusterGrouping{}) {
   cs = ClusterSet{};
   cs.leaf_cl.assign(nn, make_int2(0, 0));
   cs.leaf_sp.assign(nn, make_int2(0, 0));
@@ -95,15 +198,43 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
       }
       key[k] = {m, k};
     }
-    std::stable_sort(key.begin(), key.end(), [](const std::pair<uint32_t, int>& a,
-                                                const std::pair<uint32_t, int>& b) { return a.first < b.first; });
-    cs.leaf_cl[i] = make_int2((int)cs.info.size(), (size + CLUSTER - 1) / CLUSTER);
-    for (int b = 0; b < size; b += CLUSTER) {
-      const int cnt = std::min(CLUSTER, size - b);
+    auto by_morton = [](const std::pair<uint32_t, int>& a, const std::pair<uint32_t, int>& b) {
+      return a.first < b.first;
+    };
+    // ord: the leaf's triangles (leaf-local index) in cluster order; runs: each cluster's [begin, end) of ord
+    std::vector<int> ord(size);
+    std::vector<std::pair<int, int>> runs;
+    if (grouping.mode == 0) {
+      std::stable_sort(key.begin(), key.end(), by_morton);
+      for (int k = 0; k < size; k++) ord[k] = key[k].second;
+      for (int b = 0; b < size; b += CLUSTER) runs.push_back({b, std::min(size, b + CLUSTER)});
+    } else {
+      std::vector<std::array<double, 3>> A(size);
+      for (int k = 0; k < size; k++) {
+        const float4 a = e1[start + k], b = e2[start + k];  // glm's float edges, exact products in double
+        A[k] = {(double)a.y * b.z - (double)a.z * b.y, (double)a.z * b.x - (double)a.x * b.z,
+                (double)a.x * b.y - (double)a.y * b.x};
+        ord[k] = k;
+      }
+      std::vector<std::pair<int, int>> cones;
+      normal_cones(A, ord, 0, size, grouping, cones);
+      for (const auto& cn : cones) {
+        std::vector<std::pair<uint32_t, int>> ck;
+        for (int k = cn.first; k < cn.second; k++) ck.push_back(key[ord[k]]);
+        std::stable_sort(ck.begin(), ck.end(), by_morton);
+        for (int k = cn.first; k < cn.second; k++) ord[k] = ck[k - cn.first].second;
+        const int n = cn.second - cn.first, parts = (n + CLUSTER - 1) / CLUSTER;
+        for (int q = 0; q < parts; q++)  // balanced runs: sizes differ by at most one
+          runs.push_back({cn.first + (int)((long long)n * q / parts), cn.first + (int)((long long)n * (q + 1) / parts)});
+      }
+    }
+    cs.leaf_cl[i] = make_int2((int)cs.info.size(), (int)runs.size());
+    for (const auto& run : runs) {
+      const int b = run.first, cnt = run.second - run.first;
       float l[3] = {FLT_MAX, FLT_MAX, FLT_MAX}, h[3] = {-FLT_MAX, -FLT_MAX, -FLT_MAX};
       cs.info.push_back(make_int2((int)cs.cv0.size(), cnt));
       for (int k = b; k < b + cnt; k++) {
-        const int t = start + key[k].second;
+        const int t = start + ord[k];
         const kdpt_tri_bare& T = tris[t];
         const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
         for (int v = 0; v < 3; v++) {
@@ -127,7 +258,7 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
       const float cc[3] = {0.5f * (l[0] + h[0]), 0.5f * (l[1] + h[1]), 0.5f * (l[2] + h[2])};
       double ns[3] = {0, 0, 0};
       for (int k = b; k < b + cnt; k++) {
-        const kdpt_tri_bare& T = tris[start + key[k].second];
+        const kdpt_tri_bare& T = tris[start + ord[k]];
         const double ax = (double)T.x2 - T.x1, ay = (double)T.y2 - T.y1, az = (double)T.z2 - T.z1;
         const double bx = (double)T.x3 - T.x1, by = (double)T.y3 - T.y1, bz = (double)T.z3 - T.z1;
         ns[0] += ay * bz - az * by;
@@ -141,7 +272,7 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
         for (int a = 0; a < 3; a++) nf[a] = (float)(ns[a] / nl);
         double mn = 1e300, mx = -1e300;
         for (int k = b; k < b + cnt; k++) {
-          const kdpt_tri_bare& T = tris[start + key[k].second];
+          const kdpt_tri_bare& T = tris[start + ord[k]];
           const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
           for (int v = 0; v < 3; v++) {
             const double dv = (double)nf[0] * ((double)vx[v] - cc[0]) + (double)nf[1] * ((double)vy[v] - cc[1]) +
@@ -173,6 +304,8 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
         spread = std::max(spread, std::sqrt(cx * cx + cy * cy + cz * cz));
       }
       const float sf = std::nextafter((float)std::min(spread, 4.0), FLT_MAX);
+      cs.kc.push_back(exact_cull_coef(&cs.ce1[cs.info.back().x], &cs.ce2[cs.info.back().x], &cs.cv0[cs.info.back().x],
+                                      cnt, nl > 0 && std::isfinite(nl), nf));
       cs.lo.push_back(make_float4(l[0], l[1], l[2], dlo));
       cs.hi.push_back(make_float4(h[0], h[1], h[2], dhi));
       cs.nrm.push_back(make_float4(nf[0], nf[1], nf[2], sf));
@@ -193,7 +326,7 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
         double sx = 0, sy = 0, sxx = 0, syy = 0, sxy = 0;
         int cntv = 0;
         for (int k = b; k < b + cnt; k++) {
-          const kdpt_tri_bare& T = tris[start + key[k].second];
+          const kdpt_tri_bare& T = tris[start + ord[k]];
           const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
           for (int q = 0; q < 3; q++) {
             const double p[3] = {(double)vx[q] - cc[0], (double)vy[q] - cc[1], (double)vz[q] - cc[2]};
@@ -214,7 +347,7 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
         }
         double umn = 1e300, umx = -1e300, vmn = 1e300, vmx = -1e300;
         for (int k = b; k < b + cnt; k++) {
-          const kdpt_tri_bare& T = tris[start + key[k].second];
+          const kdpt_tri_bare& T = tris[start + ord[k]];
           const float vx[3] = {T.x1, T.x2, T.x3}, vy[3] = {T.y1, T.y2, T.y3}, vz[3] = {T.z1, T.z2, T.z3};
           for (int q = 0; q < 3; q++) {
             const double p[3] = {(double)vx[q] - cc[0], (double)vy[q] - cc[1], (double)vz[q] - cc[2]};
@@ -300,6 +433,71 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
       cs.sup_n.push_back(make_float4(nfs[0], nfs[1], nfs[2], std::nextafter((float)std::min(spread, 4.0), FLT_MAX)));
       cs.sup_b.push_back(make_float4(dmn < -1e38 ? -FLT_MAX : std::nextafter((float)dmn, -FLT_MAX),
                                      dmx > 1e38 ? FLT_MAX : std::nextafter((float)dmx, FLT_MAX), 0.0f, 0.0f));
+    }
+  }
+}
+
+// Direction masks of the exact one-level cull (DevScene::cl_mask).  For every cluster c and direction bucket b
+// (dir_bucket: a cube map of n x n cells per face) two 64-bit masks over the cluster's entries:
+//   front  (out[2 (b ncl + c)])    : the triangles that can pass glm's u/v tests for SOME direction of the
+//                                    bucket -- the others are back-facing there (float determinant < 0);
+//   danger (out[2 (b ncl + c) + 1]): those of them that can pass for a line missing the cluster's box and
+//                                    oriented box widened at the coefficient Kf: a triangle t needs the margin
+//                                    K_t(d) = 17.5 u rho_t / g_t + c (g_t = -N_t/|N_t| . d - beta_t, cull_k_exact),
+//                                    more than Kf only when g_t < 17.5 u rho_t / (Kf - c).
+// A bucket's directions d satisfy |d - d_b| <= r_b (d_b its normalised centre): the cell, grown by 1e-5 in u, v,
+// lies on the face plane at |y| >= R, where radial projection is (1/R)-Lipschitz, so r_b = half diagonal / R.
+// So |N . d - N . d_b| <= r_b (+ 1e-6 for the float d's length).  A pair whose line hits the Kf-widened boxes
+// tests its cluster's front triangles, any other pair its danger triangles; no other triangle of the cluster
+// can pass ("Cluster cull").  Exactly degenerate triangles are in both masks when |e1||e2| > 0.3
+// and in neither otherwise (their float determinant stays below FLT_EPSILON).
+constexpr int DIR_MASK_N = 16;  // default cube-map cells per face edge (6 n^2 buckets)
+inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<unsigned long long>& out) {
+  const int ncl = (int)cs.info.size(), nb = 6 * n * n;
+  out.assign(2 * (size_t)nb * ncl, 0ull);
+  const double u = ULP_HALF, grow = 1e-5;
+  for (int b = 0; b < nb; b++) {
+    const int face = b / (n * n), j = (b / n) % n, i = b % n;
+    const double a0 = -1.0 + 2.0 * i / n - grow, a1 = -1.0 + 2.0 * (i + 1) / n + grow;
+    const double b0 = -1.0 + 2.0 * j / n - grow, b1 = -1.0 + 2.0 * (j + 1) / n + grow;
+    const double ac = 0.5 * (a0 + a1), bc = 0.5 * (b0 + b1);
+    const double amin = (a0 <= 0 && a1 >= 0) ? 0.0 : std::min(std::fabs(a0), std::fabs(a1));
+    const double bmin = (b0 <= 0 && b1 >= 0) ? 0.0 : std::min(std::fabs(b0), std::fabs(b1));
+    const double R = std::sqrt(1.0 + amin * amin + bmin * bmin);
+    const double r = 0.5 * std::sqrt((a1 - a0) * (a1 - a0) + (b1 - b0) * (b1 - b0)) / R * (1.0 + 1e-9) + 1e-6;
+    double dc[3];
+    const double sgn = (face & 1) ? -1.0 : 1.0;
+    if (face < 2) { dc[0] = sgn; dc[1] = ac; dc[2] = bc; }
+    else if (face < 4) { dc[0] = ac; dc[1] = sgn; dc[2] = bc; }
+    else { dc[0] = ac; dc[1] = bc; dc[2] = sgn; }
+    const double dl = std::sqrt(dc[0] * dc[0] + dc[1] * dc[1] + dc[2] * dc[2]);
+    for (double& x : dc) x /= dl;
+    for (int c = 0; c < ncl; c++) {
+      const int2 inf = cs.info[c];
+      const double cc = cs.kc[c].w;
+      const double gden = (double)Kf - cc;
+      unsigned long long mf = 0, md = 0;
+      for (int k = 0; k < inf.y; k++) {
+        const float4 e1 = cs.ce1[inf.x + k], e2 = cs.ce2[inf.x + k];
+        const double Nx = (double)e1.y * e2.z - (double)e1.z * e2.y, Ny = (double)e1.z * e2.x - (double)e1.x * e2.z,
+                     Nz = (double)e1.x * e2.y - (double)e1.y * e2.x;
+        const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+        const double la = std::sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+        const double lb = std::sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+        if (Nl == 0.0) {
+          if (la * lb > 0.3) { mf |= 1ull << k; md |= 1ull << k; }
+          continue;
+        }
+        const double rho = std::max(1.0, la * lb / Nl);
+        const double beta = 5.8 * u * rho * (1.0 + 1e-3) + 40.0 * u;
+        const double x = (Nx * dc[0] + Ny * dc[1] + Nz * dc[2]) / Nl;
+        if (x - r > beta) continue;  // back-facing for every direction of the bucket
+        mf |= 1ull << k;
+        const double gamma = gden > 0 ? 17.5 * u * rho * (1.0 + 1e-5) / gden : 1e300;
+        if (x + r >= -beta - gamma) md |= 1ull << k;
+      }
+      out[2 * ((size_t)b * ncl + c)] = mf;
+      out[2 * ((size_t)b * ncl + c) + 1] = md;
     }
   }
 }

@@ -277,9 +277,17 @@ struct TraverseCounters {
   uint32_t aabb, tri, hit;
 };
 
-// traverseKDbareShortHybrid (HYBRID) / traverseKDbare, with the compact visited state.
-template <bool HYBRID, bool COUNT>
-KDPT_HD void traverseKD(const DevScene& S, const Ray& ray, Hit& h, int material_size, TraverseCounters& cnt) {
+// traverseKDbareShortHybrid (HYBRID) / traverseKDbare, with the compact visited state.  on_leaf(node) is
+// called for every leaf whose triangles are tested (host tools: tests/native/cull_diff.cpp --sim).
+struct NoLeafHook {
+#if defined(__HIPCC__) || defined(__HIP__)
+  __host__ __device__
+#endif
+  void operator()(int) const {}
+};
+template <bool HYBRID, bool COUNT, typename LeafHook = NoLeafHook>
+KDPT_HD void traverseKD(const DevScene& S, const Ray& ray, Hit& h, int material_size, TraverseCounters& cnt,
+                        LeafHook on_leaf = LeafHook{}) {
   if (S.num_nodes == 0) return;
   const f3 o = ray.origin, d = ray.direction;
   const f3 invdir = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -340,6 +348,7 @@ KDPT_HD void traverseKD(const DevScene& S, const Ray& ray, Hit& h, int material_
     if (L == 0) rootv = true; else cb |= 1u << lvlbit;
     const int size = meta.z;
     if (size > 0) {
+      on_leaf(cur);
       const int start = meta.y, end = start + size;
       for (int i = start; i < end; i++) {
         const float4 tv = S.tv0[i];
@@ -535,10 +544,8 @@ KDPT_HD void slab_clip(float lo, float hi, float m, float sd, float so, float& t
     tmax = fminf(tmax, fmaxf(s1, s2));
   }
 }
-KDPT_HD bool cluster_may_pass_obb(float4 lo, float4 hi, float4 n, float4 u, float4 v, float4 w, f3 o, f3 inv, f3 d,
-                                  const CullK& k) {
-  const float nd = n.x * d.x + n.y * d.y + n.z * d.z;
-  const float K = cull_margin_dir(nd, n.w, k);
+KDPT_HD bool cluster_may_pass_obb_k(float4 lo, float4 hi, float4 n, float4 u, float4 v, float4 w, f3 o, f3 inv, f3 d,
+                                    float nd, float K) {
   const float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
   const float m = K * (1.0f + fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) + (hi.x - lo.x) +
                            (hi.y - lo.y) + (hi.z - lo.z));
@@ -552,6 +559,61 @@ KDPT_HD bool cluster_may_pass_obb(float4 lo, float4 hi, float4 n, float4 u, floa
   slab_clip(u.w, w.x, m, u.x * d.x + u.y * d.y + u.z * d.z, u.x * ox + u.y * oy + u.z * oz, tmin, tmax);
   slab_clip(v.w, w.y, m, v.x * d.x + v.y * d.y + v.z * d.z, v.x * ox + v.y * oy + v.z * oz, tmin, tmax);
   return tmin <= tmax;
+}
+KDPT_HD bool cluster_may_pass_obb(float4 lo, float4 hi, float4 n, float4 u, float4 v, float4 w, f3 o, f3 inv, f3 d,
+                                  const CullK& k) {
+  const float nd = n.x * d.x + n.y * d.y + n.z * d.z;
+  return cluster_may_pass_obb_k(lo, hi, n, u, v, w, o, inv, d, nd, cull_margin_dir(nd, n.w, k));
+}
+
+// Direction buckets of the exact one-level cull (kdpt_clusters.h build_dir_masks): a cube map of n x n cells
+// per face.  The face is the largest |component| (ties: x before y before z), (u, v) the other two components
+// over it, cell (floor((u + 1) n / 2), floor((v + 1) n / 2)) clamped to n - 1.  The host bounds each cell's
+// directions (grown by 1e-5 in u and v, far above this function's rounding), so any float d maps to a cell
+// whose bound holds it.  Any finite nonzero d works (the cull only runs for lanes whose 1 / d components are
+// all finite).
+KDPT_HD int dir_bucket(f3 d, int n) {
+  const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
+  int face;
+  float a, b, m;
+  if (ax >= ay && ax >= az) {
+    face = d.x > 0.0f ? 0 : 1;
+    a = d.y;
+    b = d.z;
+    m = ax;
+  } else if (ay >= az) {
+    face = d.y > 0.0f ? 2 : 3;
+    a = d.x;
+    b = d.z;
+    m = ay;
+  } else {
+    face = d.z > 0.0f ? 4 : 5;
+    a = d.x;
+    b = d.y;
+    m = az;
+  }
+  const float h = 0.5f * (float)n / m;
+  int i = (int)((a + m) * h), j = (int)((b + m) * h);
+  i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
+  j = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
+  return (face * n + j) * n + i;
+}
+
+// The per-cluster exact margin (kdpt_clusters.h, ClusterSet::kc = {chord_eff, a, K_rig, c}) for a line of
+// direction d, nd = n . d with n the cluster's slab normal.  glm's test is single-sided: its float determinant
+// a_t = fl(e1 . (d x e2)) must reach FLT_EPSILON, and a_t is within 5.8 u |e1||e2| of -|N_t| (N_t / |N_t|) . d.
+// Every unit normal of the cluster lies within its chord of n, and chord_eff = chord (1 + 8u) + 5.8 u rho + 32 u
+// (rho: the cluster's largest |e1||e2| / |N_t|) also covers nd's rounding, so
+//   nd >  chord_eff: every a_t < 0 -- no triangle of the cluster passes: cull (returns -1);
+//   g = -nd - chord_eff > 0: a_t >= |N_t| g, so a passing point lies within 17.5 u rho / g |s| + c of the line
+//     ("Cluster cull"): K = a / g + c, at most K_rig;
+//   otherwise (a line within the chord of the cluster's patch plane): the direction-free K_rig = 8.75 E + c.
+// The floor K_lo only widens the box.
+KDPT_HD float cull_k_exact(float nd, float4 kc, float K_lo) {
+  if (nd > kc.x) return -1.0f;
+  const float g = -nd - kc.x;
+  const float K = g > 0.0f ? fminf(kc.z, kc.y / g + kc.w) : kc.z;
+  return fmaxf(K, K_lo);
 }
 
 #if defined(__HIPCC__) || defined(__HIP__)

@@ -31,6 +31,7 @@ struct Counts {
   long long lines = 0, pass = 0;           // lines tested, (line, cluster) pairs with a u/v pass
   long long culled_box = 0, viol_box = 0;  // one-level cull (dragon_5's LDS route)
   long long viol_slab = 0, viol_super = 0, viol_chunk = 0, viol_obb = 0;
+  long long viol_mask = 0, mask_items = 0;  // the exact one-level cull (build_dir_masks)
   long long nofast = 0;                    // some invdir component infinite: the wave does not cull
   long long margin_used = 0;               // passing pairs the box cull passes only thanks to the margin
   // over the passing (line, triangle) pairs: the largest distance of the line's exact crossing of the
@@ -40,6 +41,7 @@ struct Counts {
   void add(const Counts& o) {
     lines += o.lines; pass += o.pass; culled_box += o.culled_box; viol_box += o.viol_box;
     viol_slab += o.viol_slab; viol_super += o.viol_super; viol_chunk += o.viol_chunk; viol_obb += o.viol_obb;
+    viol_mask += o.viol_mask; mask_items += o.mask_items;
     nofast += o.nofast; margin_used += o.margin_used; worst = std::max(worst, o.worst);
     bound = std::max(bound, o.bound);
   }
@@ -173,6 +175,224 @@ double bound_ratio(f3 o, f3 d, float4 v0, float4 e1, float4 e2, float bx, float 
   return (double)(std::sqrt(dist2) / bound);
 }
 
+// Cull statistics of real rays through the traversal (--sim): each ray walks the tree (traverseKD, compiled
+// here for the host); for every big leaf it tests, every cluster of the leaf is evaluated with the scene-wide
+// cull the kernels ran up to round 4 (box at the scene margin + oriented box at cull_margin_dir) and with the
+// per-cluster exact cull (cull_k_exact: back-facing clusters dropped, the box and the oriented box at the
+// cluster's own margin).  A pair either cull drops while a triangle passes glm's u/v tests is a violation.
+int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_bare* tris, int nt,
+        const std::vector<float4>& tv, const std::vector<float4>& e1, const std::vector<float4>& e2,
+        const ClusterGrouping& grp) {
+  FILE* f = fopen(path, "rb");
+  if (!f) return 3;
+  std::vector<float> r;
+  float buf[6];
+  while (fread(buf, sizeof(float), 6, f) == 6) r.insert(r.end(), buf, buf + 6);
+  fclose(f);
+  const long long nr = (long long)(r.size() / 6);
+  ClusterSet cs;
+  build_cluster_set(nodes, nn, tris, tv, e1, e2, cs, grp);
+  const CullMargin cm = cluster_margin(cs.cv0, cs.ce1, cs.ce2);
+  const CullK ck{cm.K, cm.K_lo, cm.a, cm.b, cm.c};
+  std::vector<int4> nd4(4 * (size_t)nn);
+  for (int i = 0; i < nn; i++) {
+    const kdpt_node_bare& N = nodes[i];
+    nd4[4 * i] = int4{fbits(N.mins[0]), fbits(N.mins[1]), fbits(N.mins[2]), fbits(N.maxs[0])};
+    nd4[4 * i + 1] = int4{fbits(N.maxs[1]), fbits(N.maxs[2]), N.leftID, N.rightID};
+    nd4[4 * i + 2] = int4{N.parentID, N.triIdStart, N.triIdSize, N.axis};
+    nd4[4 * i + 3] = int4{0, 0, 0, 0};
+  }
+  std::vector<float4> n0(nt), n1(nt), n2(nt);
+  for (int i = 0; i < nt; i++) {
+    n0[i] = float4{tris[i].nx1, tris[i].ny1, tris[i].nz1, 0};
+    n1[i] = float4{tris[i].nx2, tris[i].ny2, tris[i].nz2, 0};
+    n2[i] = float4{tris[i].nx3, tris[i].ny3, tris[i].nz3, 0};
+  }
+  std::vector<int> offs(64, 0);
+  DevScene S{};
+  S.num_nodes = nn;
+  S.root = 0;
+  S.nodes = nd4.data();
+  S.tv0 = tv.data(); S.te1 = e1.data(); S.te2 = e2.data();
+  S.tn0 = n0.data(); S.tn1 = n1.data(); S.tn2 = n2.data();
+  S.obj_material_offsets = offs.data();
+  S.n0_left = nodes[0].leftID; S.n0_right = nodes[0].rightID;
+  S.n1_left = nn > 1 ? nodes[1].leftID : -1; S.n1_right = nn > 1 ? nodes[1].rightID : -1;
+  long long leaves = 0, pairs = 0, old_sw = 0, new_sw = 0, prod = 0, back = 0, front = 0, graze = 0, viol_old = 0,
+            viol_new = 0, nofast = 0, small_tris = 0, old_tris = 0, new_tris = 0, graze_tris = 0, ref_susp = 0,
+            ref_items = 0, ref_back = 0, ref_sw = 0, ref_tris = 0, refq_sw = 0, viol_ref = 0, cmp_rounds = 0,
+            cmp_items = 0, viol_cmp = 0, msk_items = 0, msk_pairs = 0, viol_msk = 0;
+  const int mask_n = getenv("MASK_N") ? atoi(getenv("MASK_N")) : 16;
+  std::vector<unsigned long long> masks;
+  build_dir_masks(cs, mask_n, CULL_MARGIN_FAST, masks);
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, pairs, old_sw, new_sw, prod, back, front, graze, viol_old, viol_new, nofast, small_tris, old_tris, new_tris, graze_tris, ref_susp, ref_items, ref_back, ref_sw, ref_tris, refq_sw, viol_ref, cmp_rounds, cmp_items, viol_cmp, msk_items, msk_pairs, viol_msk)
+  for (long long i = 0; i < nr; i++) {
+    const f3 o = mk3(r[6 * i], r[6 * i + 1], r[6 * i + 2]), d = mk3(r[6 * i + 3], r[6 * i + 4], r[6 * i + 5]);
+    const f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
+    const bool fast = fabsf(inv.x) < FLT_INFV && fabsf(inv.y) < FLT_INFV && fabsf(inv.z) < FLT_INFV;
+    if (!fast) nofast++;
+    std::vector<int> visited;
+    Ray ray;
+    ray.origin = o;
+    ray.direction = d;
+    ray.isinside = false;
+    ray.sdepth = 0;
+    Hit h;
+    h.t_min = FLT_MAXV; h.hit_geom_index = -1; h.obj_intersect = false; h.objMaterialIdx = -1;
+    h.ip = mk3(0, 0, 0); h.normal = mk3(0, 0, 0);
+    TraverseCounters cnt{0, 0, 0};
+    traverseKD<true, false>(S, ray, h, 1, cnt, [&](int node) {
+      if (nodes[node].triIdSize >= BIG_LEAF) visited.push_back(node);
+      else small_tris += nodes[node].triIdSize;
+    });
+    for (int node : visited) {
+      leaves++;
+      const int2 lc = cs.leaf_cl[node];
+      for (int c = lc.x; c < lc.x + lc.y; c++) {
+        pairs++;
+        const int2 inf = cs.info[c];
+        bool pass = false;
+        for (int k = 0; k < inf.y && !pass; k++) {
+          float bx, by, bz;
+          pass = tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, o, d, bx, by, bz) >= 1;
+        }
+        prod += pass;
+        if (!fast) {
+          old_sw++;
+          new_sw++;
+          continue;
+        }
+        const float4 L = cs.lo[c], H = cs.hi[c], n = cs.nrm[c];
+        const bool ok_old = cluster_may_pass(L, H, o, inv, cm.K) &&
+                            cluster_may_pass_obb(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ck);
+        const float ndv = n.x * d.x + n.y * d.y + n.z * d.z;
+        const float K = cull_k_exact(ndv, cs.kc[c], CULL_MARGIN_FAST);
+        if (K < 0) back++;
+        else if (-ndv - cs.kc[c].x > 0.0f) front++;
+        else graze++;
+        const bool ok_new = K >= 0 && cluster_may_pass(L, H, o, inv, K) &&
+                            cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, K);
+        // the refined exact cull: a fast-culled pair whose cone gives no bound is resolved per triangle (its
+        // unit normal): back-facing triangles never pass, and a front-facing one needs the margin
+        // 17.5 u rho_t / g_t + c (g_t: its determinant bound), or the rigorous one when g_t <= 0
+        {
+          const bool fast_ok = cluster_may_pass(L, H, o, inv, CULL_MARGIN_FAST) &&
+                               cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, CULL_MARGIN_FAST);
+          bool ok = fast_ok, ok_q = fast_ok;
+          if (!fast_ok && K > CULL_MARGIN_FAST) {
+            ref_susp++;
+            ref_items += inf.y;
+            double Kp = -1, Kq = -1;
+            for (int k = 0; k < inf.y; k++) {
+              const float4 a = cs.ce1[inf.x + k], b = cs.ce2[inf.x + k];
+              const double Nx = (double)a.y * b.z - (double)a.z * b.y, Ny = (double)a.z * b.x - (double)a.x * b.z,
+                           Nz = (double)a.x * b.y - (double)a.y * b.x;
+              const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+              const double la = std::sqrt((double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z);
+              const double lb = std::sqrt((double)b.x * b.x + (double)b.y * b.y + (double)b.z * b.z);
+              double Kt;
+              if (Nl == 0) {
+                if (la * lb <= 0.3) continue;
+                Kt = cs.kc[c].z;
+              } else {
+                const double rho = std::max(1.0, la * lb / Nl), u = ULP_HALF;
+                const double beta = 5.8 * u * rho * (1 + 1e-3) + 40 * u;
+                const double ndt = (Nx * d.x + Ny * d.y + Nz * d.z) / Nl;
+                if (ndt > beta) continue;  // back-facing: fl(a) < 0
+                const double g = -ndt - beta;
+                Kt = g > 0 ? std::min((double)cs.kc[c].z, 17.5 * u * rho / g + cs.kc[c].w) : cs.kc[c].z;
+              }
+              Kp = std::max(Kp, Kt);
+              const double q = Kt <= CULL_MARGIN_FAST ? CULL_MARGIN_FAST : (Kt <= 1e-3 ? 1e-3 : (Kt <= 1e-2 ? 1e-2 : (double)cs.kc[c].z));
+              Kq = std::max(Kq, q);
+            }
+            if (Kp < 0) ref_back++;
+            ok = Kp >= 0 && cluster_may_pass(L, H, o, inv, (float)std::max(Kp, 1e-4)) &&
+                 cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, (float)std::max(Kp, 1e-4));
+            ok_q = Kq >= 0 && cluster_may_pass(L, H, o, inv, (float)Kq) &&
+                   cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, (float)Kq);
+          }
+          // the compacted design: a pair not culled at the cluster level gets a normal round; every triangle
+          // that is front-facing and whose own margin reaches the pair's box is tested in full
+          {
+            const bool cheap_cull = K < 0 || (!fast_ok && K <= CULL_MARGIN_FAST) ||
+                                    !(cluster_may_pass(L, H, o, inv, cs.kc[c].z) &&
+                                      cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, cs.kc[c].z));
+            if (!cheap_cull) {
+              cmp_rounds++;
+              for (int k = 0; k < inf.y; k++) {
+                const float4 a = cs.ce1[inf.x + k], b = cs.ce2[inf.x + k];
+                const double Nx = (double)a.y * b.z - (double)a.z * b.y, Ny = (double)a.z * b.x - (double)a.x * b.z,
+                             Nz = (double)a.x * b.y - (double)a.y * b.x;
+                const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+                const double la = std::sqrt((double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z);
+                const double lb = std::sqrt((double)b.x * b.x + (double)b.y * b.y + (double)b.z * b.z);
+                double Kt;
+                if (Nl == 0) {
+                  if (la * lb <= 0.3) continue;
+                  Kt = cs.kc[c].z;
+                } else {
+                  const double rho = std::max(1.0, la * lb / Nl), u = ULP_HALF;
+                  const double beta = 5.8 * u * rho * (1 + 1e-3) + 40 * u;
+                  const double ndt = (Nx * d.x + Ny * d.y + Nz * d.z) / Nl;
+                  if (ndt > beta) continue;
+                  const double g = -ndt - beta;
+                  Kt = g > 0 ? std::min((double)cs.kc[c].z, 17.5 * u * rho / g + cs.kc[c].w) : cs.kc[c].z;
+                }
+                const float Kf = (float)std::max(Kt, (double)CULL_MARGIN_FAST);
+                const bool need = cluster_may_pass(L, H, o, inv, Kf) &&
+                                  cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, Kf);
+                cmp_items += need;
+                float bx, by, bz;
+                const bool p1 = tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, o, d, bx, by, bz) >= 1;
+                viol_cmp += p1 && !need;
+              }
+            } else {
+              viol_cmp += pass;
+            }
+          }
+          // the bucket-mask design (build_dir_masks): the pair tests its front or danger triangles
+          {
+            const int bk = dir_bucket(d, mask_n);
+            const unsigned long long mk = masks[2 * ((size_t)bk * cs.info.size() + c) + (fast_ok ? 0 : 1)];
+            msk_items += __builtin_popcountll(mk);
+            msk_pairs += mk != 0ull;
+            for (int k = 0; k < inf.y; k++) {
+              float bx, by, bz;
+              const bool p1 = tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, o, d, bx, by, bz) >= 1;
+              viol_msk += p1 && !((mk >> k) & 1ull);
+            }
+          }
+          ref_sw += ok;
+          ref_tris += ok ? inf.y : 0;
+          refq_sw += ok_q;
+          viol_ref += pass && !ok_q;
+        }
+        old_sw += ok_old;
+        new_sw += ok_new;
+        old_tris += ok_old ? inf.y : 0;
+        new_tris += ok_new ? inf.y : 0;
+        graze_tris += (ok_new && K >= 0 && !(-ndv - cs.kc[c].x > 0.0f)) ? inf.y : 0;
+        viol_old += pass && !ok_old;
+        viol_new += pass && !ok_new;
+      }
+    }
+  }
+  const double R = (double)std::max(1LL, nr);
+  printf("{\"rays\": %lld, \"clusters\": %zu, \"mode\": %d, \"chord\": %g, \"big_leaves_per_ray\": %.4f, "
+         "\"pairs_per_ray\": %.4f, \"sweeps_old\": %.4f, \"sweeps_new\": %.4f, \"productive\": %.4f, "
+         "\"back_per_ray\": %.4f, \"front_per_ray\": %.4f, \"graze_per_ray\": %.4f, \"viol_old\": %lld, "
+         "\"viol_new\": %lld, \"nofast\": %lld, \"small_tris\": %.3f, \"old_tris\": %.3f, \"new_tris\": %.3f, "
+         "\"graze_tris\": %.3f, \"ref_susp\": %.4f, \"ref_items\": %.3f, \"ref_back\": %.4f, \"ref_sweeps\": %.4f, "
+         "\"ref_tris\": %.3f, \"refq_sweeps\": %.4f, \"viol_ref\": %lld, \"cmp_rounds\": %.4f, \"cmp_items\": %.3f, "
+         "\"viol_cmp\": %lld, \"mask_n\": %d, \"msk_items\": %.3f, \"msk_pairs\": %.4f, \"viol_msk\": %lld}\n",
+         nr, cs.info.size(), grp.mode, grp.chord, leaves / R, pairs / R, old_sw / R, new_sw / R, prod / R, back / R,
+         front / R, graze / R, viol_old, viol_new, nofast, small_tris / R, old_tris / R, new_tris / R, graze_tris / R,
+         ref_susp / R, ref_items / R, ref_back / R, ref_sw / R, ref_tris / R, refq_sw / R, viol_ref, cmp_rounds / R,
+         cmp_items / R, viol_cmp, mask_n, msk_items / R, msk_pairs / R, viol_msk);
+  return 0;
+}
+
 }  // namespace
 
 int main(int argc, char** argv) {
@@ -200,6 +420,13 @@ int main(int argc, char** argv) {
     tv[i] = make_float4(T.x1, T.y1, T.z1, ibits(T.mtlIdx));
     e1[i] = make_float4(T.x2 - T.x1, T.y2 - T.y1, T.z2 - T.z1, 0.0f);
     e2[i] = make_float4(T.x3 - T.x1, T.y3 - T.y1, T.z3 - T.z1, 0.0f);
+  }
+  if (strcmp(argv[2], "--sim") == 0) {
+    ClusterGrouping grp;
+    grp.mode = argc > 4 ? atoi(argv[4]) : 0;
+    grp.chord = argc > 5 ? atof(argv[5]) : 0.5;
+    grp.min_split = argc > 6 ? atoi(argv[6]) : 8;
+    return sim(argv[3], nodes.data(), nn, tris.data(), nt, tv, e1, e2, grp);
   }
   ClusterSet cs;
   build_cluster_set(nodes.data(), nn, tris.data(), tv, e1, e2, cs);
@@ -230,6 +457,9 @@ int main(int argc, char** argv) {
   const V3 sext = shi - slo;
   const double scale = std::max(sext.x, std::max(sext.y, sext.z));
 
+  const int mask_n = getenv("MASK_N") ? atoi(getenv("MASK_N")) : DIR_MASK_N;
+  std::vector<unsigned long long> masks;
+  build_dir_masks(cs, mask_n, CULL_MARGIN_FAST, masks);
   Counts tot[NGEN];
   const int nthreads = 1;
 #pragma omp parallel
@@ -374,6 +604,22 @@ int main(int argc, char** argv) {
       }
       const bool box = cluster_may_pass(L, H, of, inv, K);
       if (!box) C.culled_box++;
+      {
+        // the exact one-level cull: the cluster's front mask when the line hits the Kf-widened box and
+        // oriented box, else its danger mask; every triangle passing glm's u/v tests must be in it
+        const float ndv = cs.nrm[c].x * df.x + cs.nrm[c].y * df.y + cs.nrm[c].z * df.z;
+        const bool hit = cluster_may_pass(L, H, of, inv, CULL_MARGIN_FAST) &&
+                         cluster_may_pass_obb_k(L, H, cs.nrm[c], cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], of, inv, df, ndv,
+                                                CULL_MARGIN_FAST);
+        const unsigned long long mk = masks[2 * ((size_t)dir_bucket(df, mask_n) * ncl + c) + (hit ? 0 : 1)];
+        C.mask_items += __builtin_popcountll(mk);
+        for (int k = 0; k < inf.y; k++) {
+          float bx, by, bz;
+          if (tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, of, df, bx, by, bz) >= 1 &&
+              !((mk >> k) & 1ull))
+            C.viol_mask++;
+        }
+      }
       if (pass) {
         C.pass++;
         if (!box) C.viol_box++;
@@ -407,12 +653,14 @@ int main(int argc, char** argv) {
     const Counts& C = tot[g];
     all.add(C);
     printf("%s\"%s\": {\"lines\": %lld, \"pass\": %lld, \"culled_box\": %lld, \"viol_box\": %lld, \"viol_slab\": %lld, "
-           "\"viol_super\": %lld, \"viol_chunk\": %lld, \"viol_obb\": %lld, \"nofast\": %lld, \"margin_used\": %lld, \"worst\": %.4g, \"bound\": %.4g}",
+           "\"viol_super\": %lld, \"viol_chunk\": %lld, \"viol_obb\": %lld, \"viol_mask\": %lld, \"mask_items\": %lld, "
+           "\"nofast\": %lld, \"margin_used\": %lld, \"worst\": %.4g, \"bound\": %.4g}",
            g ? ", " : "", kGenName[g], C.lines, C.pass, C.culled_box, C.viol_box, C.viol_slab, C.viol_super,
-           C.viol_chunk, C.viol_obb, C.nofast, C.margin_used, C.worst, C.bound);
+           C.viol_chunk, C.viol_obb, C.viol_mask, C.mask_items, C.nofast, C.margin_used, C.worst, C.bound);
   }
-  printf("}, \"violations\": %lld, \"lines\": %lld, \"pass\": %lld, \"margin_used\": %lld, \"worst\": %.4g, \"bound\": %.4g}\n",
-         all.viol_box + all.viol_slab + all.viol_super + all.viol_chunk + all.viol_obb, all.lines, all.pass, all.margin_used,
-         all.worst, all.bound);
+  printf("}, \"violations\": %lld, \"viol_mask\": %lld, \"lines\": %lld, \"pass\": %lld, \"margin_used\": %lld, "
+         "\"worst\": %.4g, \"bound\": %.4g}\n",
+         all.viol_box + all.viol_slab + all.viol_super + all.viol_chunk + all.viol_obb, all.viol_mask, all.lines, all.pass,
+         all.margin_used, all.worst, all.bound);
   return 0;
 }
