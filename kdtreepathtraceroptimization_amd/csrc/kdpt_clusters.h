@@ -12,6 +12,7 @@
 #include <array>
 #include <cfloat>
 #include <cmath>
+#include <thread>
 #include <utility>
 #include <vector>
 
@@ -286,8 +287,10 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
       }
       // the spread of the triangles' normals about nf (slab level's direction-dependent margin,
       // cull_margin_dir): the largest chord |N_t / |N_t| - nf| over the cluster, N_t = e1 x e2 of glm's float
-      // edges, rounded up; 4 (never a usable lower bound) when nf = 0 or a triangle is a sliver
-      // (|e1| |e2| / |N_t| > CULL_RHO_CAP) that could still pass glm's determinant test
+      // edges, rounded up; 4 (never a usable lower bound) when nf = 0, when a triangle is a sliver
+      // (|e1| |e2| / |N_t| > CULL_RHO_CAP: the scene-wide rho of cull_margin_dir leaves it out, so only the
+      // direction-free margin covers it), or when an exactly degenerate triangle has |e1||e2| > 0.3 (below that
+      // its float determinant stays under FLT_EPSILON: it never passes)
       double spread = (nl > 0 && std::isfinite(nl)) ? 0.0 : 4.0;
       for (int k = b; k < b + cnt && spread < 4.0; k++) {
         const int e = cs.info.back().x + (k - b);
@@ -296,10 +299,11 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
         const double Nx = ay * bz - az * by, Ny = az * bx - ax * bz, Nz = ax * by - ay * bx;
         const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
         const double E = std::sqrt(ax * ax + ay * ay + az * az) * std::sqrt(bx * bx + by * by + bz * bz);
-        if (Nl == 0.0 || E > CULL_RHO_CAP * Nl) {
-          if (E > 0.3) spread = 4.0;  // (|a| <= 5.8 u E < FLT_EPSILON otherwise: it never passes)
+        if (Nl == 0.0 ? E > 0.3 : E > CULL_RHO_CAP * Nl) {
+          spread = 4.0;
           continue;
         }
+        if (Nl == 0.0) continue;
         const double cx = Nx / Nl - nf[0], cy = Ny / Nl - nf[1], cz = Nz / Nl - nf[2];
         spread = std::max(spread, std::sqrt(cx * cx + cy * cy + cz * cz));
       }
@@ -413,9 +417,9 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
           const double Nx = ay * bz - az * by, Ny = az * bx - ax * bz, Nz = ax * by - ay * bx;
           const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
           const double E = std::sqrt(ax * ax + ay * ay + az * az) * std::sqrt(bx * bx + by * by + bz * bz);
-          if (Nl == 0.0 || E > CULL_RHO_CAP * Nl) {
-            if (E > 0.3) spread = 4.0;
-          } else if (spread < 4.0) {
+          if (Nl == 0.0 ? E > 0.3 : E > CULL_RHO_CAP * Nl) {
+            spread = 4.0;  // (as the clusters' spread: a sliver, or a degenerate triangle that can pass)
+          } else if (Nl > 0.0 && spread < 4.0) {
             const double cx = Nx / Nl - nfs[0], cy = Ny / Nl - nfs[1], cz = Nz / Nl - nfs[2];
             spread = std::max(spread, std::sqrt(cx * cx + cy * cy + cz * cz));
           }
@@ -438,10 +442,10 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
 }
 
 // Direction masks of the exact one-level cull (DevScene::cl_mask).  For every cluster c and direction bucket b
-// (dir_bucket: a cube map of n x n cells per face) two 64-bit masks over the cluster's entries:
-//   front  (out[2 (b ncl + c)])    : the triangles that can pass glm's u/v tests for SOME direction of the
+// (dir_bucket: a cube map of n x n cells per face, nb = 6 n^2 buckets) two 64-bit masks over its entries:
+//   front  (out[2 (c nb + b)])     : the triangles that can pass glm's u/v tests for SOME direction of the
 //                                    bucket -- the others are back-facing there (float determinant < 0);
-//   danger (out[2 (b ncl + c) + 1]): those of them that can pass for a line missing the cluster's box and
+//   danger (out[2 (c nb + b) + 1]): those of them that can pass for a line missing the cluster's box and
 //                                    oriented box widened at the coefficient Kf: a triangle t needs the margin
 //                                    K_t(d) = 17.5 u rho_t / g_t + c (g_t = -N_t/|N_t| . d - beta_t, cull_k_exact),
 //                                    more than Kf only when g_t < 17.5 u rho_t / (Kf - c).
@@ -456,6 +460,40 @@ inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<u
   const int ncl = (int)cs.info.size(), nb = 6 * n * n;
   out.assign(2 * (size_t)nb * ncl, 0ull);
   const double u = ULP_HALF, grow = 1e-5;
+  // per entry (structure of arrays): the unit normal and the two thresholds on x = N . d_b -- front when
+  // x - r <= beta, danger when also x + r >= dthr.  Entries in both masks always get (0, inf, -inf), entries in
+  // neither (padding, exactly degenerate with |e1||e2| <= 0.3) (0, -inf, -)
+  const size_t ne = 64 * (size_t)ncl;
+  std::vector<double> nx(ne, 0.0), ny(ne, 0.0), nz(ne, 0.0), beta(ne, -HUGE_VAL), dthr(ne, HUGE_VAL);
+  for (int c = 0; c < ncl; c++) {
+    const int2 inf = cs.info[c];
+    const double gden = (double)Kf - cs.kc[c].w;
+    for (int k = 0; k < inf.y; k++) {
+      const size_t q = 64 * (size_t)c + k;
+      const float4 e1 = cs.ce1[inf.x + k], e2 = cs.ce2[inf.x + k];
+      const double Nx = (double)e1.y * e2.z - (double)e1.z * e2.y, Ny = (double)e1.z * e2.x - (double)e1.x * e2.z,
+                   Nz = (double)e1.x * e2.y - (double)e1.y * e2.x;
+      const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+      const double la = std::sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+      const double lb = std::sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+      if (Nl == 0.0) {
+        if (la * lb > 0.3) {
+          beta[q] = HUGE_VAL;
+          dthr[q] = -HUGE_VAL;
+        }
+        continue;
+      }
+      const double rho = std::max(1.0, la * lb / Nl);
+      nx[q] = Nx / Nl;
+      ny[q] = Ny / Nl;
+      nz[q] = Nz / Nl;
+      beta[q] = 5.8 * u * rho * (1.0 + 1e-3) + 40.0 * u;
+      const double gamma = gden > 0 ? 17.5 * u * rho * (1.0 + 1e-5) / gden : HUGE_VAL;
+      dthr[q] = -beta[q] - gamma;
+    }
+  }
+  // the buckets' centre directions and radii
+  std::vector<double> bd(4 * (size_t)nb);
   for (int b = 0; b < nb; b++) {
     const int face = b / (n * n), j = (b / n) % n, i = b % n;
     const double a0 = -1.0 + 2.0 * i / n - grow, a1 = -1.0 + 2.0 * (i + 1) / n + grow;
@@ -464,42 +502,47 @@ inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<u
     const double amin = (a0 <= 0 && a1 >= 0) ? 0.0 : std::min(std::fabs(a0), std::fabs(a1));
     const double bmin = (b0 <= 0 && b1 >= 0) ? 0.0 : std::min(std::fabs(b0), std::fabs(b1));
     const double R = std::sqrt(1.0 + amin * amin + bmin * bmin);
-    const double r = 0.5 * std::sqrt((a1 - a0) * (a1 - a0) + (b1 - b0) * (b1 - b0)) / R * (1.0 + 1e-9) + 1e-6;
-    double dc[3];
+    double* D = &bd[4 * (size_t)b];
+    D[3] = 0.5 * std::sqrt((a1 - a0) * (a1 - a0) + (b1 - b0) * (b1 - b0)) / R * (1.0 + 1e-9) + 1e-6;
     const double sgn = (face & 1) ? -1.0 : 1.0;
-    if (face < 2) { dc[0] = sgn; dc[1] = ac; dc[2] = bc; }
-    else if (face < 4) { dc[0] = ac; dc[1] = sgn; dc[2] = bc; }
-    else { dc[0] = ac; dc[1] = bc; dc[2] = sgn; }
-    const double dl = std::sqrt(dc[0] * dc[0] + dc[1] * dc[1] + dc[2] * dc[2]);
-    for (double& x : dc) x /= dl;
-    for (int c = 0; c < ncl; c++) {
-      const int2 inf = cs.info[c];
-      const double cc = cs.kc[c].w;
-      const double gden = (double)Kf - cc;
-      unsigned long long mf = 0, md = 0;
-      for (int k = 0; k < inf.y; k++) {
-        const float4 e1 = cs.ce1[inf.x + k], e2 = cs.ce2[inf.x + k];
-        const double Nx = (double)e1.y * e2.z - (double)e1.z * e2.y, Ny = (double)e1.z * e2.x - (double)e1.x * e2.z,
-                     Nz = (double)e1.x * e2.y - (double)e1.y * e2.x;
-        const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
-        const double la = std::sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
-        const double lb = std::sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
-        if (Nl == 0.0) {
-          if (la * lb > 0.3) { mf |= 1ull << k; md |= 1ull << k; }
-          continue;
-        }
-        const double rho = std::max(1.0, la * lb / Nl);
-        const double beta = 5.8 * u * rho * (1.0 + 1e-3) + 40.0 * u;
-        const double x = (Nx * dc[0] + Ny * dc[1] + Nz * dc[2]) / Nl;
-        if (x - r > beta) continue;  // back-facing for every direction of the bucket
-        mf |= 1ull << k;
-        const double gamma = gden > 0 ? 17.5 * u * rho * (1.0 + 1e-5) / gden : 1e300;
-        if (x + r >= -beta - gamma) md |= 1ull << k;
-      }
-      out[2 * ((size_t)b * ncl + c)] = mf;
-      out[2 * ((size_t)b * ncl + c) + 1] = md;
-    }
+    if (face < 2) { D[0] = sgn; D[1] = ac; D[2] = bc; }
+    else if (face < 4) { D[0] = ac; D[1] = sgn; D[2] = bc; }
+    else { D[0] = ac; D[1] = bc; D[2] = sgn; }
+    const double dl = std::sqrt(D[0] * D[0] + D[1] * D[1] + D[2] * D[2]);
+    for (int a = 0; a < 3; a++) D[a] /= dl;
   }
+  // cluster-major (out[2 (c nb + b)] front, + 1 danger): a cluster's 64 entries stay in cache over its buckets
+  auto work = [&](int c) {
+    const size_t q0 = 64 * (size_t)c;
+    for (int b = 0; b < nb; b++) {
+      const double* D = &bd[4 * (size_t)b];
+      unsigned long long mf = 0, md = 0;
+      for (int k = 0; k < 64; k++) {
+        const size_t q = q0 + k;
+        const double x = nx[q] * D[0] + ny[q] * D[1] + nz[q] * D[2];
+        const bool f = x - D[3] <= beta[q];  // else back-facing for every direction of the bucket
+        mf |= (unsigned long long)f << k;
+        md |= (unsigned long long)(f && x + D[3] >= dthr[q]) << k;
+      }
+      out[2 * ((size_t)c * nb + b)] = mf;
+      out[2 * ((size_t)c * nb + b) + 1] = md;
+    }
+  };
+  const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
+  std::vector<std::thread> th;
+  for (int t = 0; t < nth; t++)
+    th.emplace_back([&, t]() {
+      for (int c = t; c < ncl; c += nth) work(c);
+    });
+  for (auto& x : th) x.join();
+}
+
+// The cube-map resolution of the masks: the finest of 32 / 16 / 8 / 4 / 2 cells per face edge whose masks
+// (16 bytes per cluster and bucket) fit in `budget` bytes.
+inline int dir_mask_resolution(int ncl, size_t budget = (size_t)32 << 20) {
+  for (int n : {32, 16, 8, 4})
+    if ((size_t)ncl * 6 * n * n * 16 <= budget) return n;
+  return 2;
 }
 
 // The brute-force route's boxes of 64 file-order triangles [64j, 64j + 64): the triangles glm tests,

@@ -147,6 +147,11 @@ struct DevScene {
   // the slab level uses cull_margin_dir(): max(cl_margin_lo, min(cl_margin, cull_a / g + cull_c)),
   // g = |n . d| - cl_n.w - cull_b
   float cl_margin, cl_margin_lo, cull_a, cull_b, cull_c;
+  // the exact one-level cull (kdpt_clusters.h build_dir_masks): per cluster c and direction bucket b,
+  // cl_mask[c * 6 mask_n^2 + b] = {front, danger} masks over the cluster's 64 entries; null: the fast-margin
+  // cull (tuning "cull_exact" = 0) or no one-level cull at all
+  const ulonglong2* cl_mask;
+  int mask_n;  // cube-map cells per face edge (dir_bucket)
   const int4* snodes;
   const float4* c_v0;
   const float4* c_e1;
@@ -925,6 +930,27 @@ __device__ inline float bpermute_f(float v, int src_lane) {
   return __int_as_float(__builtin_amdgcn_ds_bpermute(src_lane << 2, __float_as_int(v)));
 }
 
+// Position of the j-th (0-based) set bit of m (j < popcount(m)): a 6-step bisection on popcounts.
+__device__ inline int select_bit(unsigned long long m, int j) {
+  uint32_t x = (uint32_t)m;
+  int base = 0, c = __popc(x);
+  if (j >= c) {
+    j -= c;
+    x = (uint32_t)(m >> 32);
+    base = 32;
+  }
+#pragma unroll
+  for (int w = 16; w >= 1; w >>= 1) {
+    c = __popc(x & ((1u << w) - 1u));
+    if (j >= c) {
+      j -= c;
+      x >>= w;
+      base += w;
+    }
+  }
+  return base;
+}
+
 // Owner lane of pair B + lane in a flattened (lane, item) enumeration where lane L owns pairs
 // [excl_L, excl_L + cnt_L) (lanes in order, so starts increase with L).  The segment starts inside the
 // window [B, B + 64) are scattered into slot[] (lane + 1), an inclusive max-scan fills the gaps, and a
@@ -1180,7 +1206,108 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   // one is tested.  Recombination by ORIGINAL index into the owner lane (order-free): last u/v pass = max
   // index, last hit = max, best = min (t, index).
   const bool big = leaf && lsize >= BIG_LEAF;
-  if (__any(big)) {
+  bool big_done = false;
+  if constexpr (!ClusterSrc::kSuper) {
+    if (S.cl_mask && __any(big)) {
+      // The exact one-level cull.  Pass: 64 (ray, cluster) pairs, lane = pair; the pair's line against the
+      // cluster's box and oriented box widened at the fast coefficient (cl_margin).  A hit selects the cluster's
+      // front mask for the ray's direction bucket, a miss its danger mask (build_dir_masks: every triangle
+      // that can pass glm's u/v tests is in the selected mask).  Then the (pair, masked triangle) items of the
+      // pass, 64 per round, lane = item, its ray from the owner's LDS slot; the results recombine on the ray's
+      // LDS slots by original index (order-free), as in the small leaves.
+      const int ncl = big ? (lsize + CLUSTER - 1) / CLUSTER : 0;
+      const int cfirst = big ? (NodeSrc::kLeafHoldsCluster ? lstart : S.leaf_cl[lnode].x) : 0;
+      const int incl = wave_incl_scan<false>(ncl);
+      const int P = __builtin_amdgcn_readlane(incl, 63);
+      const int excl = incl - ncl;
+      W->tbase[lane] = cfirst - excl;  // cluster of pair q = tbase[owner] + q
+      W->lastPass[lane] = 0ull;
+      W->lastHit[lane] = -1;
+      W->nhit[lane] = 0;
+      W->best[lane] = ~0ull;
+      wave_lds_sync();
+      if (COUNT) {
+        prof_add(WP, PROF_BIG_LEAVES, (unsigned long long)__popcll(__ballot(big)));
+        prof_add(WP, PROF_BIG_CLUSTERS, (unsigned long long)P);
+      }
+      int carry = 0;
+      for (int B = 0; B < P; B += 64) {
+        const int own = pair_owner(W->slot, excl, ncl, B, carry);
+        const int c = W->tbase[own] + B + lane;
+        const bool valid = B + lane < P;
+        unsigned long long m = valid ? ~0ull : 0ull;  // no cull: every entry (padding fails glm's determinant)
+        if (fastAABB) {
+          const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
+          const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
+          const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
+          ulonglong2 mm = make_ulonglong2(0ull, 0ull);
+          float4 clo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), chi = clo;
+          bool hit = false;
+          if (valid) {
+            mm = S.cl_mask[(size_t)c * (6 * S.mask_n * S.mask_n) + dir_bucket(dd, S.mask_n)];
+            clo = clusters.lo_of(c);
+            chi = clusters.hi_of(c);
+            hit = cluster_may_pass(clo, chi, oo, ii, S.cl_margin);
+          }
+          if (S.flat_obb && __any(hit)) {
+            if (hit) {
+              const float4 cn = S.cl_n[c];
+              hit = cluster_may_pass_obb_k(clo, chi, cn, S.cl_u[c], S.cl_v[c], S.cl_w[c], oo, ii, dd,
+                                           cn.x * dd.x + cn.y * dd.y + cn.z * dd.z, S.cl_margin);
+            }
+          }
+          m = valid ? (hit ? mm.x : mm.y) : 0ull;
+        }
+        if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
+        const int ni = __popcll(m);
+        const int iincl = wave_incl_scan<false>(ni);
+        const int Q = __builtin_amdgcn_readlane(iincl, 63);
+        const int iexcl = iincl - ni;
+        int icarry = 0;
+        for (int Rb = 0; Rb < Q; Rb += 64) {
+          if (COUNT) prof_add(WP, PROF_BIG_SWEEPS, 1);
+          const int pl = pair_owner(W->slot, iexcl, ni, Rb, icarry);
+          const int rank = Rb + lane - __builtin_amdgcn_ds_bpermute(pl << 2, iexcl);
+          const unsigned long long ml =
+              ((unsigned long long)(uint32_t)__builtin_amdgcn_ds_bpermute(pl << 2, (int)(uint32_t)(m >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_ds_bpermute(pl << 2, (int)(uint32_t)m);
+          const int cl = __builtin_amdgcn_ds_bpermute(pl << 2, c);
+          const int rl = __builtin_amdgcn_ds_bpermute(pl << 2, own);  // the pair's ray: lane rl's
+          if (Rb + lane < Q) {
+            const int e = cl * 64 + select_bit(ml, rank);
+            const TriData T{S.c_v0[e], S.c_e1[e], S.c_e2[e]};
+            const float4 q0 = W->od[rl];
+            const float2 q1 = W->dd[rl];
+            const f3 ro = mk3(q0.x, q0.y, q0.z), rd = mk3(q0.w, q1.x, q1.y);
+            const int orig = fbits(T.e1.w);
+            float bx, by, bzk;
+            const int r = tri_test_v(T, ro, rd, bx, by, bzk);
+            if (r >= 1) atomicMax(&W->lastPass[rl], ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk));
+            if (r == 2) {
+              atomicMax(&W->lastHit[rl], orig);
+              atomicAdd(&W->nhit[rl], 1);
+              f3 hp, nn;
+              const float t = tri_hit_t<HYBRID>(S, orig, ro, rd, bx, by, bzk, hp, nn);
+              if (t > 0.0f) atomicMin(&W->best[rl], ((unsigned long long)f2u(t) << 32) | (unsigned int)orig);
+            }
+          }
+        }
+        if (COUNT) prof_lap(WP, PROF_BIG_CYC);
+      }
+      wave_lds_sync();
+      if (big) {
+        const unsigned long long lp = W->lastPass[lane];
+        r_pass = (int)(lp >> 32);
+        r_bz = u2f((uint32_t)(lp & 0xffffffffu));
+        r_lasthit = W->lastHit[lane];
+        r_nhit = W->nhit[lane];
+        r_best = W->best[lane];
+      }
+      wave_lds_sync();  // the LDS slots are rewritten by the small leaves
+      big_done = true;
+    }
+  }
+  if (!big_done && __any(big)) {
     unsigned long long k_pass = 0ull, k_best = ~0ull;
     int k_lasthit = -1, k_nhit = 0;
     // Sweeps of the (ray, cluster) pairs `pass` marks: cluster c with the ray of lane own, each surviving

@@ -27,6 +27,7 @@
 struct float4 { float x, y, z, w; };
 struct int4 { int x, y, z, w; };
 struct int2 { int x, y; };
+struct ulonglong2 { unsigned long long x, y; };
 static inline int4 make_int4(int x, int y, int z, int w) { return int4{x, y, z, w}; }
 static inline float4 make_float4(float x, float y, float z, float w) { return float4{x, y, z, w}; }
 static inline int2 make_int2(int x, int y) { return int2{x, y}; }

@@ -21,6 +21,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <memory>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -1691,6 +1692,13 @@ struct kdpt_ctx {
   bool force_global_tree = false;  // "tree_global" tuning knob: keep the tree in HBM/L2
   bool super_cull = true;          // "super_cull" tuning knob: 0 = no TREE_LDS16S route (one-level cull)
   CullMargin cull{};                // the scene's cluster-cull margins (kdpt_clusters.h cluster_margin)
+  // the exact one-level cull's direction masks (kdpt_clusters.h build_dir_masks), built when the scene's rigorous
+  // margin is above the cap; S.cl_mask points at them unless a knob chose another cull
+  ulonglong2* mask_dev = nullptr;
+  int mask_n = 0;
+  bool cull_exact = true;   // "cull_exact" knob: 0 = the fast-margin cull (not exact for such scenes)
+  bool cull_scene = true;   // false after "cluster_cull" = 0 or a fixed "cull_margin"
+  std::unique_ptr<ClusterSet> mask_cs;  // the clusters the masks were built from ("cull_mask_n" rebuilds)
   int tree_format = 0;             // "tree_format" knob: 16 / 32 = LDS node records of that size only
   size_t tree_lds = 0;    // dynamic LDS bytes of the intersect kernel (TREE_LDS)
   int* tile_counts = nullptr;
@@ -1963,6 +1971,24 @@ void set_cull(kdpt_ctx* c, const CullMargin& cm) {
 void fix_cull(kdpt_ctx* c, float K) {
   c->S.cl_margin = c->S.cl_margin_lo = K;
 }
+// The one-level route's cull: the exact masked one when the scene has masks and the knobs leave the scene's
+// margins in place, else the margin-only cull.
+void apply_cull_route(kdpt_ctx* c) {
+  c->S.cl_mask = (c->mask_dev && c->cull_exact && c->cull_scene) ? c->mask_dev : nullptr;
+  c->S.mask_n = c->mask_n;
+}
+// The direction masks of the scene's clusters at resolution n (cube-map cells per face edge), uploaded.
+int build_masks(kdpt_ctx* c, int n) {
+  std::vector<unsigned long long> m;
+  build_dir_masks(*c->mask_cs, n, c->cull.K, m);
+  ulonglong2* d = nullptr;
+  int rc = dupload(c, &d, reinterpret_cast<const ulonglong2*>(m.data()), m.size() / 2);
+  if (rc) return rc;
+  c->mask_dev = d;
+  c->mask_n = n;
+  apply_cull_route(c);
+  return KDPT_OK;
+}
 
 // Big leaves as clusters of <= 64 triangles, super-clusters and slabs (kdpt_clusters.h), uploaded.
 int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>& tv, const std::vector<float4>& e1,
@@ -2003,6 +2029,12 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
   c->S.sup_b = dsb;
   c->S.sup_slab = 1;
   set_cull(c, cluster_margin(cv0, ce1, ce2));
+  // no margin makes the cull exact for these triangles: the masked one-level cull (its direction masks for the
+  // fast margin the box levels use)
+  if (!c->cull.exact && !info.empty()) {
+    c->mask_cs.reset(new ClusterSet(cs));
+    if ((rc = build_masks(c, dir_mask_resolution((int)info.size())))) return rc;
+  }
   c->S.sup = dsp;
   // a super box past the half range (+-65504) would be infinite, its centre NaN and the cull wrong: such a
   // scene gets no super-cluster route (TREE_LDS16S needs num_supers > 0)
@@ -2135,7 +2167,8 @@ int setup_trace(kdpt_ctx* c) {
       if (st16 + t16 + cl_bytes <= lds_max) cands.push_back({TREE_LDS16, t16 + cl_bytes});
       // (leaving room for a fused-shading workgroup's LDS beside the intersect workgroup)
       const size_t sp_bytes = 16 * (size_t)c->S.num_supers;
-      if (c->S.snodes && c->super_cull && st16 + t16 + sp_bytes + SHADE_LDS_RESERVE <= lds_max)
+      // (not when the one-level cull is the masked exact one: the supers' margins are not rigorous for it)
+      if (c->S.snodes && c->super_cull && !c->S.cl_mask && st16 + t16 + sp_bytes + SHADE_LDS_RESERVE <= lds_max)
         cands.push_back({TREE_LDS16S, t16 + sp_bytes});
       if (st16 + t16 <= lds_max) cands.push_back({TREE_LDS16G, t16});
     }
@@ -2632,15 +2665,33 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     int rc = setup_trace(c);
     if (rc) return rc;
     if (c->grid_env) c->trace_grid = std::max(1, (int)(c->full_trace_grid * frac));
-  } else if (k == "cluster_cull") {
-    // 0: no cluster / chunk cull at all (every big-leaf cluster swept: exact by construction, whatever the
-    // scene's margin); 1: the scene's margin
-    if (v != 0) set_cull(c, c->cull);
-    else fix_cull(c, __builtin_inff());
-  } else if (k == "cull_margin") {
-    if (!(value >= 0.0)) return fail(KDPT_ERR_ARG, "cull_margin must be >= 0 (0: the scene's)");
-    if (value > 0.0) fix_cull(c, (float)value);
-    else set_cull(c, c->cull);
+  } else if (k == "cluster_cull" || k == "cull_margin" || k == "cull_exact" || k == "cull_mask_n") {
+    if (k == "cluster_cull") {
+      // 0: no cluster / chunk cull at all (every big-leaf cluster swept: exact by construction, whatever the
+      // scene's margin); 1: the scene's margins (and masks)
+      c->cull_scene = v != 0;
+      if (v != 0) set_cull(c, c->cull);
+      else fix_cull(c, __builtin_inff());
+    } else if (k == "cull_margin") {
+      // > 0: one fixed margin coefficient for every level (no masks: not exact in general); 0: the scene's
+      if (!(value >= 0.0)) return fail(KDPT_ERR_ARG, "cull_margin must be >= 0 (0: the scene's)");
+      c->cull_scene = value == 0.0;
+      if (value > 0.0) fix_cull(c, (float)value);
+      else set_cull(c, c->cull);
+    } else if (k == "cull_exact") {
+      // 0: the fast-margin one-level cull instead of the masked exact one (A/B; not exact for such scenes)
+      c->cull_exact = v != 0;
+    } else {
+      if (v != 2 && v != 4 && v != 8 && v != 16 && v != 32) return fail(KDPT_ERR_ARG, "cull_mask_n must be 2, 4, 8, 16 or 32");
+      if (!c->mask_cs) return fail(KDPT_ERR_ARG, "cull_mask_n: this scene has no direction masks");
+      int rc = build_masks(c, v);
+      if (rc) return rc;
+    }
+    apply_cull_route(c);
+    const double frac = (double)c->trace_grid / std::max(1, c->full_trace_grid);
+    int rc = setup_trace(c);  // the route may change (no super-cluster route under the masked cull)
+    if (rc) return rc;
+    if (c->grid_env) c->trace_grid = std::max(1, (int)(c->full_trace_grid * frac));
   } else if (k == "profile_batches") {
     c->profile_batches = v != 0;
     c->profile_steps = v >= 2;
@@ -2854,8 +2905,9 @@ int kdpt_cull_margin(kdpt_ctx* c, float* margin, double* rigorous, int* exact) {
   if (!c) return fail(KDPT_ERR_ARG, "null ctx");
   if (margin) *margin = c->S.cl_margin;
   if (rigorous) *rigorous = c->cull.rigorous;
-  // the box-only levels use cl_margin; the slab level's margin is rigorous by construction whenever that is
-  if (exact) *exact = (double)c->S.cl_margin >= c->cull.rigorous ? 1 : 0;
+  // the box-only levels use cl_margin; the slab level's margin is rigorous by construction whenever that is;
+  // the masked one-level cull is exact whatever the margin (its masks hold every triangle that can pass)
+  if (exact) *exact = ((double)c->S.cl_margin >= c->cull.rigorous || c->S.cl_mask) ? 1 : 0;
   return KDPT_OK;
 }
 

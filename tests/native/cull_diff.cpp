@@ -354,7 +354,7 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
           // the bucket-mask design (build_dir_masks): the pair tests its front or danger triangles
           {
             const int bk = dir_bucket(d, mask_n);
-            const unsigned long long mk = masks[2 * ((size_t)bk * cs.info.size() + c) + (fast_ok ? 0 : 1)];
+            const unsigned long long mk = masks[2 * ((size_t)c * 6 * mask_n * mask_n + bk) + (fast_ok ? 0 : 1)];
             msk_items += __builtin_popcountll(mk);
             msk_pairs += mk != 0ull;
             for (int k = 0; k < inf.y; k++) {
@@ -611,7 +611,7 @@ int main(int argc, char** argv) {
         const bool hit = cluster_may_pass(L, H, of, inv, CULL_MARGIN_FAST) &&
                          cluster_may_pass_obb_k(L, H, cs.nrm[c], cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], of, inv, df, ndv,
                                                 CULL_MARGIN_FAST);
-        const unsigned long long mk = masks[2 * ((size_t)dir_bucket(df, mask_n) * ncl + c) + (hit ? 0 : 1)];
+        const unsigned long long mk = masks[2 * ((size_t)c * 6 * mask_n * mask_n + dir_bucket(df, mask_n)) + (hit ? 0 : 1)];
         C.mask_items += __builtin_popcountll(mk);
         for (int k = 0; k < inf.y; k++) {
           float bx, by, bz;

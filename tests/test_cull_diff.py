@@ -55,9 +55,30 @@ def trees(tmp_path_factory):
     return get
 
 
-def run(exe, *args):
-    r = subprocess.run([exe, *map(str, args)], check=True, capture_output=True, text=True, timeout=600)
+def run(exe, *args, env=None):
+    r = subprocess.run([exe, *map(str, args)], check=True, capture_output=True, text=True, timeout=600,
+                       env=None if env is None else {**os.environ, **env})
     return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+@pytest.fixture(scope="module")
+def rays_c3(tmp_path_factory):
+    """Rays of a real C3 render (the oracle's paths after bounces 0-6 of iteration 3 at 800x800), a seeded
+    sample of 150 000, as float32 origin.xyz, direction.xyz."""
+    import sys
+    sys.path.insert(0, os.path.join(REPO, "tests"))
+    import oracle_lib
+    from kdtreepathtraceroptimization_amd import load_fixture_scene
+    s = oracle_lib.OracleScene.from_description(load_fixture_scene("cornell", "dragon_5", res=(800, 800), depth=8))
+    rays = []
+    for sd in range(7):
+        p = s.paths_after(3, sd)
+        rays.append(np.concatenate([p["origin"], p["direction"]], axis=1).astype(np.float32))
+    rays = np.concatenate(rays)
+    pick = np.random.default_rng(5).choice(len(rays), size=min(150_000, len(rays)), replace=False)
+    path = str(tmp_path_factory.mktemp("rays") / "rays.bin")
+    rays[np.sort(pick)].tofile(path)
+    return path
 
 
 def test_c5_margin_is_rigorous_and_never_drops_a_pass(cull_diff, trees):
@@ -84,39 +105,83 @@ def test_rigorous_margin_never_drops_a_pass(cull_diff, trees, mesh):
 
 
 def test_fast_margin_is_not_rigorous_for_large_triangles(cull_diff, trees):
-    """dragon_5 with the fast margin the kernels use for it (1e-4; kdpt_cull_margin reports exact = 0): the
-    derived error bound still holds for every pass, and the rounding-targeted generator does construct lines
-    the fast cull drops while a triangle passes glm's u/v tests -- lines lying in a triangle's plane (to within
-    rounding), within ~1e-5 rad of parallel to it, passing beside the cluster's box.  This is what the
-    rigorous margin and the cluster_cull knob exist for; the harness is sensitive enough to see it."""
+    """dragon_5 with the fast margin alone (1e-4; the route of the "cull_exact" = 0 knob): the derived error
+    bound still holds for every pass, and the rounding-targeted generator does construct lines the fast box
+    cull drops while a triangle passes glm's u/v tests -- lines lying in a triangle's plane (to within rounding),
+    within ~1e-5 rad of parallel to it, passing beside the cluster's box.  The same lines keep every such
+    triangle in the direction mask the default (masked) cull selects: zero mask violations."""
     r = run(cull_diff, trees("dragon_5"), 2_000_000, 47)
     assert r["exact"] == 0 and r["margin"] < r["rigorous"], r
     assert 0 < r["bound"] <= 1.0, r
     rnd = r["gens"]["round"]
     assert rnd["viol_box"] > 0, r
+    assert r["viol_mask"] == 0, r
     # everything else (random lines, lines grazing at >= 1e-7.5 rad through the plane's own float points,
     # box faces, axis directions) stays clean at this margin
     for g in ("random", "face", "axis"):
         assert r["gens"][g]["viol_box"] + r["gens"][g]["viol_slab"] + r["gens"][g]["viol_super"] == 0, (g, r)
 
 
-def test_real_rays_never_hit_a_dropped_pass(cull_diff, trees, tmp_path):
-    """Rays of a real C3 render (the oracle's paths after bounces 0-6 of iteration 3 at 800x800, a seeded
-    sample of 150 000) against EVERY cluster of dragon_5 (not only those the traversal visits), at the fast
+@pytest.mark.parametrize("mesh,n", [("dragon_5", 32), ("dragon_5", 16), ("dragon_5", 4), ("dragon_3", 32),
+                                    ("icosphere_7", 8)])
+def test_direction_masks_never_drop_a_pass(cull_diff, trees, mesh, n):
+    """The masked one-level cull (kdpt_clusters.h build_dir_masks; the default for every scene whose rigorous
+    margin is above the cap): for every adversarial line, every triangle that passes glm's u/v tests is in the
+    mask the kernel selects (front mask when the line hits the cluster's fast-margin box and oriented box,
+    danger mask otherwise), at several cube-map resolutions."""
+    r = run(cull_diff, trees(mesh), 3_000_000 if mesh == "dragon_5" else 1_000_000, 53 + n, env={"MASK_N": str(n)})
+    assert r["viol_mask"] == 0, r
+    assert r["pass"] > 50_000, r
+    assert r["gens"]["round"]["pass"] > 0, r
+
+
+def test_real_rays_through_the_traversal_keep_every_pass(cull_diff, trees, rays_c3):
+    """Rays of a real C3 render walked through the traversal (tests/native/cull_diff.cpp --sim): at every big
+    leaf they visit, no cluster triangle that passes glm's u/v tests is left out of the selected mask, and the
+    masked cull tests about as many triangles per ray as the fast one swept (no perf cliff: at most 1.5x)."""
+    r = run(cull_diff, trees("dragon_5"), "--sim", rays_c3, 0, env={"MASK_N": "32"})
+    assert r["viol_msk"] == 0 and r["viol_old"] == 0, r
+    assert r["big_leaves_per_ray"] > 0.1, r
+    assert r["msk_items"] <= 1.5 * r["sweeps_old"] * 64, r
+
+
+def test_slivers_force_the_direction_free_margin(cull_diff, tmp_path):
+    """a sliver (|e1||e2| > 64 |e1 x e2|) that can still pass glm's determinant test sets its
+    cluster's (and super's) normal spread to 4, so the slab levels fall back to the rigorous direction-free
+    margin.  An icosphere small enough for the rigorous margin (level 7, radius 1: exact = 1) with 1 in 16
+    triangles pinched into slivers of rho ~ 50-400: no cull level drops a pass."""
+    from kdtreepathtraceroptimization_amd import SceneData, load_fixture_scene
+    from kdtreepathtraceroptimization_amd.meshes import dragon_material, icosphere_unit
+    u = icosphere_unit(7)
+    tri = u * 1.0 + np.array([0.0, 2.0, 0.0])
+    k = np.arange(len(tri))
+    eps = np.where(k % 32 == 0, 5e-3, 2e-2)[:, None]
+    sl = k % 16 == 0  # (a, b, b + eps (c - b)): |N| ~ eps |N_abc|, |e1||e2| ~ |e1|^2
+    tri[sl, 2] = tri[sl, 1] + eps[sl] * (tri[sl, 2] - tri[sl, 1])
+    desc = load_fixture_scene("cornell", None, res=(64, 64))
+    desc.verts9 = tri.astype(np.float32).reshape(-1, 9)
+    desc.norms9 = np.repeat(_unit_rows(u), 1, axis=0).astype(np.float32).reshape(-1, 9)
+    desc.shape_of_tri = np.zeros(len(tri), np.int32)
+    desc.shape_materials = dragon_material()
+    sd = SceneData.from_description(desc)
+    path = str(tmp_path / "sliver.bin")
+    with open(path, "wb") as f:
+        f.write(struct.pack("<ii", sd.view.num_nodes, sd.view.num_tris))
+        f.write(sd.nodes_bytes())
+        f.write(sd.tris_bytes())
+    r = run(cull_diff, path, 3_000_000, 61)
+    assert r["exact"] == 1, r
+    assert r["violations"] == 0 and r["viol_mask"] == 0, r
+    assert r["pass"] > 50_000, r
+
+
+def _unit_rows(u):
+    return u / np.linalg.norm(u, axis=-1, keepdims=True)
+
+
+def test_real_rays_never_hit_a_dropped_pass(cull_diff, trees, rays_c3):
+    """The same rays against EVERY cluster of dragon_5 (not only those the traversal visits), at the fast
     margin: no cull level drops a pair with a u/v pass."""
-    import sys
-    sys.path.insert(0, os.path.join(REPO, "tests"))
-    import oracle_lib
-    from kdtreepathtraceroptimization_amd import load_fixture_scene
-    s = oracle_lib.OracleScene.from_description(load_fixture_scene("cornell", "dragon_5", res=(800, 800), depth=8))
-    rays = []
-    for sd in range(7):
-        p = s.paths_after(3, sd)
-        rays.append(np.concatenate([p["origin"], p["direction"]], axis=1).astype(np.float32))
-    rays = np.concatenate(rays)
-    pick = np.random.default_rng(5).choice(len(rays), size=min(150_000, len(rays)), replace=False)
-    path = str(tmp_path / "rays.bin")
-    rays[np.sort(pick)].tofile(path)
-    r = run(cull_diff, trees("dragon_5"), "--rays", path)
-    assert r["rays"] == len(pick) and r["pairs"] > 10_000_000, r
+    r = run(cull_diff, trees("dragon_5"), "--rays", rays_c3)
+    assert r["rays"] == 150_000 and r["pairs"] > 10_000_000, r
     assert r["violations"] == 0, r
