@@ -212,7 +212,7 @@ def main():
             dist.init_process_group("gloo")
     from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options, load_fixture_scene
     from kdtreepathtraceroptimization_amd.distributed import frame_share
-    from kdtreepathtraceroptimization_amd.runtime import comm_unique_id
+    from kdtreepathtraceroptimization_amd.runtime import comm_library, comm_unique_id
 
     # a step is one frame: weak scaling renders spp-per-step samples per GPU per frame, strong scaling a fixed
     # --total-spp per frame split over the GPUs
@@ -230,6 +230,7 @@ def main():
     # the process group), or -- gloo rehearsals, ranks sharing a GPU -- each rank's frame shares handed out
     # and reduced here over gloo
     gloo = dist is not None and args.dist_backend == "gloo"
+    rccl_lib = None
     if dist is not None:
         if gloo:
             pt.comm_init(world, rank, None)
@@ -237,6 +238,7 @@ def main():
             ids = [comm_unique_id() if rank == 0 else None]
             dist.broadcast_object_list(ids, src=0)
             pt.comm_init(world, rank, ids[0])
+            rccl_lib = comm_library()  # the librccl the library's reduces actually go through
 
     # warmup: frames disjoint from the timed ones (iteration 2's extra sort lands here)
     shares = torch.empty((args.steps, 3 * W * H), dtype=torch.float32, device=f"cuda:{local}") if gloo else None
@@ -354,7 +356,9 @@ def main():
                    "parallelism": (f"spp-sharded x{world}, one framebuffer reduce per frame: "
                                    + ("RCCL ncclReduce inside libkdpt (kdpt_render_frames)"
                                       if args.dist_backend == "nccl" else "gloo host reduce (ranks sharing GPUs)"))
-                   if world > 1 else "single GPU"},
+                   if world > 1 else ("single GPU, one-rank RCCL communicator: ncclReduce per frame inside libkdpt"
+                                      if dist is not None and not gloo else "single GPU"),
+                   **({"rccl_library": rccl_lib} if rccl_lib else {})},
         "ms_per_iteration": round(dt * 1e3 * world / iters, 4),
         "segments_per_iteration": round(seg / iters, 1),
         "primary_rays_per_s": round(W * H * iters / dt, 1),

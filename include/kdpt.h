@@ -275,10 +275,15 @@ int kdpt_cull_margin(kdpt_ctx *ctx, float *margin, double *rigorous, int *exact)
  * communicator; kdpt_render_frames then copies every rank's frame shares to its `out` and the caller reduces
  * them (e.g. over gloo when ranks share a GPU, which RCCL refuses); the image is left alone. */
 int kdpt_comm_unique_id(unsigned char *id);
+/* id given: a communicator for any nranks >= 1 (one rank runs the same per-frame ncclReduce as N). */
 int kdpt_comm_init(kdpt_ctx *ctx, int nranks, int rank, const unsigned char *id);
+/* The path of the RCCL library whose ncclReduce the calls use (dladdr; in a torch process torch's copy when
+ * it was loaded first).  KDPT_ERR_UNSUPPORTED when no librccl.so.1 can be loaded. */
+int kdpt_comm_library(char *path, int len);
 /* This rank's share of frames first_frame .. first_frame + frames - 1 (every rank calls it with the same
  * arguments); out: rank 0, frames * 3*W*H floats, device or host memory, or NULL. */
 int kdpt_render_frames(kdpt_ctx *ctx, int first_frame, int frames, int spp, int pipeline, int batch, float *out);
+/* (a pageable host `out` is pinned for the copies -- hipHostRegister -- until kdpt_synchronize) */
 /* One process, one context per device (devices[0..ndev), <= 8; a device may repeat with KDPT_REDUCE_COPY):
  * renders the frames, waits, and frees everything.  out (host or device 0 memory, frames * 3*W*H floats, or
  * NULL) receives each frame's reduced image. */

@@ -1764,6 +1764,7 @@ struct kdpt_ctx {
   hipEvent_t frame_ev[2] = {nullptr, nullptr};      // frame_buf[k] consumed by its reduce
   hipEvent_t frame_acc_ev[2] = {nullptr, nullptr};  // frame_buf[k]'s accumulations done
   hipStream_t reduce_stream = nullptr;  // the frames' reduces and image adds, beside the accumulation stream
+  std::vector<void*> host_reg;  // pageable host `out` ranges pinned for kdpt_render_frames (released at synchronize)
 };
 
 namespace {
@@ -1787,6 +1788,7 @@ int dupload(kdpt_ctx* c, T** p, const T* src, size_t n) {
 
 int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count);
 void release_comm(kdpt_ctx* c);  // (multi-GPU section, end of file)
+void unregister_host(kdpt_ctx* c);
 int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, int stop_depth, bool count,
                  std::vector<hipEvent_t>* bev);
 
@@ -2736,6 +2738,8 @@ int kdpt_synchronize(kdpt_ctx* c) {
     if (rc) return rc;
   }
   if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
+  if (c->reduce_stream) HIP_TRY(hipStreamSynchronize(c->reduce_stream));
+  unregister_host(c);
   int rc = drain_intersect_events(c);
   if (rc) return rc;
   if (c->profile_batches) HIP_TRY(hipMemcpy(&c->last_profile, c->counters, sizeof(Counters), hipMemcpyDeviceToHost));
@@ -3018,8 +3022,11 @@ int kdpt_destroy(kdpt_ctx* c) {
   for (auto& evs : c->pending_ev)
     for (auto e : evs) (void)hipEventDestroy(e);
   for (auto e : c->free_ev) (void)hipEventDestroy(e);
-  release_comm(c);
+  // (a kdpt_render_frames that failed partway may have left a reduce queued: drain it before the communicator
+  // and the frame buffers go)
   if (c->reduce_stream) (void)hipStreamSynchronize(c->reduce_stream);
+  release_comm(c);
+  unregister_host(c);
   for (auto e : c->frame_ev)
     if (e) (void)hipEventDestroy(e);
   for (auto e : c->frame_acc_ev)
@@ -3596,6 +3603,11 @@ void release_comm(kdpt_ctx* c) {
   c->owns_comm = false;
 }
 
+void unregister_host(kdpt_ctx* c) {
+  for (void* p : c->host_reg) (void)hipHostUnregister(p);
+  c->host_reg.clear();
+}
+
 int frame_buffers(kdpt_ctx* c) {
   const size_t n3 = 3 * (size_t)c->npix;
   if (!c->reduce_stream) HIP_TRY(hipStreamCreateWithFlags(&c->reduce_stream, hipStreamNonBlocking));
@@ -3610,6 +3622,18 @@ int frame_buffers(kdpt_ctx* c) {
   }
   if (!c->frame_sum && c->rank == 0) return dalloc(c, &c->frame_sum, n3);
   return KDPT_OK;
+}
+
+// A pageable host `out` is pinned in place for the frames' copies (hipHostRegister), so they run as queued
+// instead of staging synchronously at every frame's enqueue (which would serialise frame f + 1's enqueue behind
+// frame f's reduce); device memory, already pinned memory and failed registrations are left as they are.
+void pin_host_out(kdpt_ctx* c, void* p, size_t bytes) {
+  if (!p || !bytes) return;
+  hipPointerAttribute_t a;
+  if (hipPointerGetAttributes(&a, p) == hipSuccess && a.type != hipMemoryTypeUnregistered) return;
+  (void)hipGetLastError();
+  if (hipHostRegister(p, bytes, hipHostRegisterDefault) == hipSuccess) c->host_reg.push_back(p);
+  else (void)hipGetLastError();
 }
 
 // Iterations of frame f for rank r of n: first, stride n, count.
@@ -3652,6 +3676,17 @@ int check_frames_args(kdpt_ctx* c, int first_frame, int frames, int spp) {
 
 }  // namespace
 
+int kdpt_comm_library(char* path, int len) {
+  if (!path || len < 1) return fail(KDPT_ERR_ARG, "bad arguments");
+  const Rccl* R = rccl();
+  if (!R) return fail(KDPT_ERR_UNSUPPORTED, "librccl.so.1 not found");
+  // the file that actually provides ncclReduce (in a torch process: torch's own librccl, if loaded first)
+  Dl_info info{};
+  const char* f = dladdr(reinterpret_cast<void*>(R->reduce), &info) && info.dli_fname ? info.dli_fname : "?";
+  snprintf(path, (size_t)len, "%s", f);
+  return KDPT_OK;
+}
+
 int kdpt_comm_unique_id(unsigned char* id) {
   if (!id) return fail(KDPT_ERR_ARG, "null id");
   const Rccl* R = rccl();
@@ -3674,7 +3709,9 @@ int kdpt_comm_init(kdpt_ctx* c, int nranks, int rank, const unsigned char* id) {
   c->nranks = nranks;
   c->rank = rank;
   c->external_reduce = nranks > 1 && !id;
-  if (nranks > 1 && id) {
+  // (one rank with an id gets a communicator too: kdpt_render_frames then runs the same ncclReduce per frame
+  // as on N GPUs, so one GPU exercises the multi-GPU path end to end)
+  if (id) {
     if (!R) return fail(KDPT_ERR_UNSUPPORTED, "librccl.so.1 not found");
     ncclUniqueId u;
     memcpy(&u, id, sizeof u);
@@ -3693,6 +3730,7 @@ int kdpt_render_frames(kdpt_ctx* c, int first_frame, int frames, int spp, int pi
   const Rccl* R = c->comm ? rccl() : nullptr;
   if (c->nranks > 1 && !R && !c->external_reduce) return fail(KDPT_ERR_ARG, "kdpt_comm_init first");
   const size_t n3 = 3 * (size_t)c->npix;
+  if (c->rank == 0 || c->external_reduce) pin_host_out(c, out, sizeof(float) * n3 * (size_t)frames);
   for (int k = 0; k < frames; k++) {
     const int f = first_frame + k;
     if ((rc = enqueue_frame(c, f, spp, pipeline, batch))) return rc;
@@ -3706,7 +3744,7 @@ int kdpt_render_frames(kdpt_ctx* c, int first_frame, int frames, int spp, int pi
     if (c->external_reduce) {  // the caller reduces: every rank's share goes out as it is
       if (out) HIP_TRY(hipMemcpyAsync(out + (size_t)k * n3, fb, sizeof(float) * n3, hipMemcpyDefault, rs));
     } else {
-      if (c->nranks > 1) {
+      if (R) {
         RCCL_TRY(R, R->reduce(fb, c->rank == 0 ? c->frame_sum : nullptr, n3, ncclFloat32, ncclSum, 0,
                               (ncclComm_t)c->comm, rs));
         sum = c->frame_sum;
@@ -3731,9 +3769,15 @@ int kdpt_render_sharded(const kdpt_scene* scene, const kdpt_options* opt, int nd
   else kdpt_default_options(&o);
   o.external_image = nullptr;
   std::vector<kdpt_ctx*> cs(ndev, nullptr);
+  // every event this call records across devices (destroyed once the contexts' streams are drained)
+  std::vector<std::pair<int, hipEvent_t>> xev;
   auto cleanup = [&](int rc) {
     for (auto c : cs)
-      if (c) kdpt_destroy(c);  // (releases its communicator)
+      if (c) kdpt_destroy(c);  // (drains its streams, releases its communicator)
+    for (auto& de : xev) {
+      (void)hipSetDevice(de.first);
+      (void)hipEventDestroy(de.second);
+    }
     return rc;
   };
   int rc;
@@ -3760,11 +3804,26 @@ int kdpt_render_sharded(const kdpt_scene* scene, const kdpt_options* opt, int nd
   if (reduce == KDPT_REDUCE_COPY)
     for (int i = 1; i < ndev; i++)
       if ((rc = dalloc(c0, &staged[i], (size_t)n3))) return cleanup(rc);
+  // a pageable host `out` pinned for the call (released by the final kdpt_synchronize of c0)
+  pin_host_out(c0, out, sizeof(float) * (size_t)n3 * (size_t)frames);
+  auto xevent = [&](int dev, hipStream_t st, hipEvent_t* e) {
+    if (hipSetDevice(dev) != hipSuccess || hipEventCreateWithFlags(e, hipEventDisableTiming) != hipSuccess ||
+        hipEventRecord(*e, st) != hipSuccess)
+      return false;
+    xev.push_back({dev, *e});
+    return true;
+  };
   for (int k = 0; k < frames; k++) {
     const int f = first_frame + k;
+    // each rank queues its share on its accumulation stream; its reduce stream waits for the share (as in
+    // kdpt_render_frames), so frame f + 1's accumulations never queue behind frame f's reduce
     for (int i = 0; i < ndev; i++) {
-      if (hipSetDevice(cs[i]->device) != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "hipSetDevice"));
-      if ((rc = enqueue_frame(cs[i], f, spp, pipeline, batch))) return cleanup(rc);
+      kdpt_ctx* ci = cs[i];
+      if (hipSetDevice(ci->device) != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "hipSetDevice"));
+      if ((rc = enqueue_frame(ci, f, spp, pipeline, batch))) return cleanup(rc);
+      if (hipEventRecord(ci->frame_acc_ev[f & 1], ci->accum_stream) != hipSuccess ||
+          hipStreamWaitEvent(ci->reduce_stream, ci->frame_acc_ev[f & 1], 0) != hipSuccess)
+        return cleanup(fail(KDPT_ERR_HIP, "frame events"));
     }
     if (hipSetDevice(c0->device) != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "hipSetDevice"));
     if ((rc = frame_buffers(c0))) return cleanup(rc);
@@ -3773,43 +3832,39 @@ int kdpt_render_sharded(const kdpt_scene* scene, const kdpt_options* opt, int nd
       ncclResult_t e = ncclSuccess;
       for (int i = 0; i < ndev && e == ncclSuccess; i++)
         e = R->reduce(cs[i]->frame_buf[f & 1], i == 0 ? c0->frame_sum : nullptr, (size_t)n3, ncclFloat32, ncclSum,
-                      0, (ncclComm_t)cs[i]->comm, cs[i]->accum_stream);
+                      0, (ncclComm_t)cs[i]->comm, cs[i]->reduce_stream);
       const ncclResult_t e2 = R->groupEnd();
       if (e != ncclSuccess || e2 != ncclSuccess)
         return cleanup(fail(KDPT_ERR_HIP, std::string("rccl: ") + R->errorString(e != ncclSuccess ? e : e2)));
     } else {
-      // device 0 waits for every rank's frame, copies the others' over (peer copies: xGMI between GPUs)
+      // device 0's reduce stream waits for every rank's share and copies the others' over (peer copies: xGMI
+      // between GPUs), then adds them in rank order
       FrameParts parts{};
       parts.n = ndev;
       parts.p[0] = c0->frame_buf[f & 1];
       for (int i = 1; i < ndev; i++) {
         kdpt_ctx* ci = cs[i];
-        hipEvent_t ready;
-        if (hipSetDevice(ci->device) != hipSuccess || hipEventCreateWithFlags(&ready, hipEventDisableTiming) != hipSuccess ||
-            hipEventRecord(ready, ci->accum_stream) != hipSuccess || hipSetDevice(c0->device) != hipSuccess ||
-            hipStreamWaitEvent(c0->accum_stream, ready, 0) != hipSuccess ||
+        if (hipSetDevice(c0->device) != hipSuccess ||
+            hipStreamWaitEvent(c0->reduce_stream, ci->frame_acc_ev[f & 1], 0) != hipSuccess ||
             hipMemcpyPeerAsync(staged[i], c0->device, ci->frame_buf[f & 1], ci->device, sizeof(float) * (size_t)n3,
-                               c0->accum_stream) != hipSuccess)
+                               c0->reduce_stream) != hipSuccess)
           return cleanup(fail(KDPT_ERR_HIP, "copy reduce"));
-        (void)hipEventDestroy(ready);  // (released once recorded work completes)
         parts.p[i] = staged[i];
       }
-      hipLaunchKernelGGL(k_sum_frames, dim3((n3 + 255) / 256), dim3(256), 0, c0->accum_stream, c0->frame_sum, parts, n3);
+      hipLaunchKernelGGL(k_sum_frames, dim3((n3 + 255) / 256), dim3(256), 0, c0->reduce_stream, c0->frame_sum, parts, n3);
       if (hipGetLastError() != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "k_sum_frames"));
       // the other ranks' frame_buf[f & 1] may be reused (frame f + 2) once these copies are done
-      for (int i = 1; i < ndev; i++) {
-        hipEvent_t done;
-        if (hipEventCreateWithFlags(&done, hipEventDisableTiming) != hipSuccess ||
-            hipEventRecord(done, c0->accum_stream) != hipSuccess || hipSetDevice(cs[i]->device) != hipSuccess ||
-            hipStreamWaitEvent(cs[i]->accum_stream, done, 0) != hipSuccess || hipSetDevice(c0->device) != hipSuccess)
+      hipEvent_t done;
+      if (!xevent(c0->device, c0->reduce_stream, &done)) return cleanup(fail(KDPT_ERR_HIP, "copy reduce"));
+      for (int i = 1; i < ndev; i++)
+        if (hipSetDevice(cs[i]->device) != hipSuccess || hipStreamWaitEvent(cs[i]->reduce_stream, done, 0) != hipSuccess)
           return cleanup(fail(KDPT_ERR_HIP, "copy reduce"));
-        (void)hipEventDestroy(done);
-      }
     }
-    if ((rc = finish_frame(c0, c0->frame_sum, out, k, c0->accum_stream))) return cleanup(rc);
+    if (hipSetDevice(c0->device) != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "hipSetDevice"));
+    if ((rc = finish_frame(c0, c0->frame_sum, out, k, c0->reduce_stream))) return cleanup(rc);
     for (int i = 0; i < ndev; i++) {
       if (hipSetDevice(cs[i]->device) != hipSuccess ||
-          hipEventRecord(cs[i]->frame_ev[f & 1], cs[i]->accum_stream) != hipSuccess)
+          hipEventRecord(cs[i]->frame_ev[f & 1], cs[i]->reduce_stream) != hipSuccess)
         return cleanup(fail(KDPT_ERR_HIP, "hipEventRecord"));
     }
   }

@@ -115,6 +115,7 @@ EXPORTS = [
     "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm", "kdpt_set_options", "kdpt_scene_build_device",
     "kdpt_scene_kd_build_ms", "kdpt_build_kd_device", "kdpt_scene_load_device", "kdpt_trace_config",
     "kdpt_cull_margin", "kdpt_comm_unique_id", "kdpt_comm_init", "kdpt_render_frames", "kdpt_render_sharded",
+    "kdpt_comm_library",
 ]
 
 REDUCE_RCCL, REDUCE_COPY = 0, 1  # kdpt_render_sharded's reduce (KDPT_REDUCE_*)
@@ -164,6 +165,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     if hasattr(lib, "kdpt_render_frames"):
         lib.kdpt_comm_unique_id.argtypes = [C.c_void_p]
         lib.kdpt_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
+        if hasattr(lib, "kdpt_comm_library"):
+            lib.kdpt_comm_library.argtypes = [C.c_char_p, C.c_int]
         lib.kdpt_render_frames.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_int, C.c_int, C.c_void_p]
         lib.kdpt_render_sharded.argtypes = [P(Scene), P(Options), C.c_int, P(C.c_int), C.c_int, C.c_int, C.c_int,
                                             C.c_int, C.c_int, C.c_int, C.c_void_p]
@@ -576,6 +579,14 @@ def imgsum(image: np.ndarray) -> float:
 
 
 COMM_ID_BYTES = 128
+
+
+def comm_library() -> str:
+    """kdpt_comm_library: the RCCL library file the library's reduces go through."""
+    lib = load_library()
+    buf = C.create_string_buffer(4096)
+    _check(lib.kdpt_comm_library(buf, 4096), "kdpt_comm_library")
+    return buf.value.decode(errors="replace")
 
 
 def comm_unique_id() -> bytes:

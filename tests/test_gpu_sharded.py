@@ -198,6 +198,51 @@ def test_render_frames_one_rank_equals_trace_iterations():
     assert np.array_equal(img.view(np.uint32), (out[0] + out[1]).view(np.uint32))
 
 
+@pytest.mark.parametrize("spp", [5, 12, 32])
+def test_render_sharded_copy_eight_ranks(spp):
+    """kdpt_render_sharded with eight contexts (all on this box's one GPU, the in-process copy reduce): the C++
+    frame_share at N = 8 -- with spp 5 ranks 5-7 render nothing, and iteration 2 (the sort) falls on rank 1 --
+    and every frame equals the eight ranks' shares added in rank order, bit for bit."""
+    from functools import reduce as fold
+
+    from kdtreepathtraceroptimization_amd import SceneData
+    from kdtreepathtraceroptimization_amd.runtime import REDUCE_COPY, render_sharded
+    sd = SceneData.from_description(load_fixture_scene("cornell8", "dragon_5", res=(96, 72), depth=8))
+    frames, devices = 2, [0] * 8
+    got = render_sharded(sd, devices, 0, frames, spp, pipeline=2, batch=2, reduce=REDUCE_COPY)
+    for f in range(frames):
+        parts = _frame_parts(sd, f, spp, len(devices))
+        expect = fold(np.add, parts)
+        assert np.array_equal(got[f].view(np.uint32), expect.view(np.uint32)), f"frame {f}"
+
+
+def test_render_frames_one_rank_rccl_equals_trace_iterations():
+    """kdpt_comm_init with an id at one rank makes a real communicator, so kdpt_render_frames runs
+    the per-frame ncclReduce, frame_sum, the reduce stream's ordering and the communicator's destruction on
+    one GPU -- and the frames still equal kdpt_trace_iterations bit for bit (a one-rank reduce is a copy)."""
+    from kdtreepathtraceroptimization_amd import PathTracer, SceneData, default_options
+    from kdtreepathtraceroptimization_amd.runtime import comm_library, comm_unique_id
+    sd = SceneData.from_description(load_fixture_scene("cornell", "dragon_5", res=(200, 160), depth=8))
+    spp = 6
+    with PathTracer(sd, default_options(), device=0) as ref:
+        ref.trace_iterations(1, 2 * spp, pipeline=3, batch=2)
+        ref.synchronize()
+        two = ref.image()
+    assert "rccl" in comm_library()
+    with PathTracer(sd, default_options(), device=0) as pt:
+        pt.comm_init(1, 0, comm_unique_id())
+        out = np.zeros((2, 160, 200, 3), np.float32)
+        pt.render_frames(0, 2, spp, pipeline=3, batch=2, out=out)  # pageable host out: pinned by the library
+        pt.synchronize()
+        img = pt.image()
+    f0 = _frame_parts(sd, 0, spp, 1)[0]
+    f1 = _frame_parts(sd, 1, spp, 1)[0]
+    assert np.array_equal(out[0].view(np.uint32), f0.view(np.uint32))
+    assert np.array_equal(out[1].view(np.uint32), f1.view(np.uint32))
+    assert np.array_equal(img.view(np.uint32), (f0 + f1).view(np.uint32))
+    assert np.allclose(img, two, rtol=1e-6, atol=1e-5)  # (frame sums vs one running sum: rounding only)
+
+
 @pytest.mark.parametrize("reduce", ["copy", "rccl"])
 def test_render_sharded_equals_rank_parts(reduce):
     """kdpt_render_sharded, one process, one context per device: with RCCL on this box's one GPU (one
