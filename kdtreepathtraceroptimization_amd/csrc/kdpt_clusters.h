@@ -442,27 +442,25 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
 }
 
 // Direction masks of the exact one-level cull (DevScene::cl_mask).  For every cluster c and direction bucket b
-// (dir_bucket: a cube map of n x n cells per face, nb = 6 n^2 buckets) two 64-bit masks over its entries:
-//   front  (out[2 (c nb + b)])     : the triangles that can pass glm's u/v tests for SOME direction of the
-//                                    bucket -- the others are back-facing there (float determinant < 0);
-//   danger (out[2 (c nb + b) + 1]): those of them that can pass for a line missing the cluster's box and
-//                                    oriented box widened at the coefficient Kf: a triangle t needs the margin
-//                                    K_t(d) = 17.5 u rho_t / g_t + c (g_t = -N_t/|N_t| . d - beta_t, cull_k_exact),
-//                                    more than Kf only when g_t < 17.5 u rho_t / (Kf - c).
+// (dir_bucket: a cube map of n x n cells per face, nb = 6 n^2 buckets), out[c nb + b] = the danger mask over the
+// cluster's 64 entries: the triangles that, for SOME direction of the bucket, are front-facing and need a margin
+// above Kf -- the coefficient of the fast box test a pair's line missed.  A triangle t needs the margin
+// K_t(d) = 17.5 u rho_t / g_t + c (g_t = -N_t/|N_t| . d - beta_t; danger_needs_test), above Kf only when
+// g_t < 17.5 u rho_t / (Kf - c).  Every other triangle of such a cluster is back-facing for the whole bucket
+// (its float determinant negative) or lies farther from the line than its own error bound: it cannot pass glm's
+// u/v tests ("Cluster cull").
 // A bucket's directions d satisfy |d - d_b| <= r_b (d_b its normalised centre): the cell, grown by 1e-5 in u, v,
 // lies on the face plane at |y| >= R, where radial projection is (1/R)-Lipschitz, so r_b = half diagonal / R.
-// So |N . d - N . d_b| <= r_b (+ 1e-6 for the float d's length).  A pair whose line hits the Kf-widened boxes
-// tests its cluster's front triangles, any other pair its danger triangles; no other triangle of the cluster
-// can pass ("Cluster cull").  Exactly degenerate triangles are in both masks when |e1||e2| > 0.3
-// and in neither otherwise (their float determinant stays below FLT_EPSILON).
-constexpr int DIR_MASK_N = 16;  // default cube-map cells per face edge (6 n^2 buckets)
+// So |N . d - N . d_b| <= r_b (+ 1e-6 for the float d's length).  Exactly degenerate triangles are in every mask
+// when |e1||e2| > 0.3 and in none otherwise (their float determinant stays below FLT_EPSILON).
+constexpr int DIR_MASK_N = 32;  // default cube-map cells per face edge (6 n^2 buckets)
 inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<unsigned long long>& out) {
   const int ncl = (int)cs.info.size(), nb = 6 * n * n;
-  out.assign(2 * (size_t)nb * ncl, 0ull);
+  out.assign((size_t)nb * ncl, 0ull);
   const double u = ULP_HALF, grow = 1e-5;
   // per entry (structure of arrays): the unit normal and the two thresholds on x = N . d_b -- front when
-  // x - r <= beta, danger when also x + r >= dthr.  Entries in both masks always get (0, inf, -inf), entries in
-  // neither (padding, exactly degenerate with |e1||e2| <= 0.3) (0, -inf, -)
+  // x - r <= beta, danger when also x + r >= dthr.  Entries in every mask get (0, inf, -inf), entries in none
+  // (padding, exactly degenerate with |e1||e2| <= 0.3) (0, -inf, -)
   const size_t ne = 64 * (size_t)ncl;
   std::vector<double> nx(ne, 0.0), ny(ne, 0.0), nz(ne, 0.0), beta(ne, -HUGE_VAL), dthr(ne, HUGE_VAL);
   for (int c = 0; c < ncl; c++) {
@@ -511,21 +509,19 @@ inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<u
     const double dl = std::sqrt(D[0] * D[0] + D[1] * D[1] + D[2] * D[2]);
     for (int a = 0; a < 3; a++) D[a] /= dl;
   }
-  // cluster-major (out[2 (c nb + b)] front, + 1 danger): a cluster's 64 entries stay in cache over its buckets
+  // cluster-major: a cluster's 64 entries stay in cache over its buckets
   auto work = [&](int c) {
     const size_t q0 = 64 * (size_t)c;
     for (int b = 0; b < nb; b++) {
       const double* D = &bd[4 * (size_t)b];
-      unsigned long long mf = 0, md = 0;
+      unsigned long long md = 0;
       for (int k = 0; k < 64; k++) {
         const size_t q = q0 + k;
         const double x = nx[q] * D[0] + ny[q] * D[1] + nz[q] * D[2];
-        const bool f = x - D[3] <= beta[q];  // else back-facing for every direction of the bucket
-        mf |= (unsigned long long)f << k;
-        md |= (unsigned long long)(f && x + D[3] >= dthr[q]) << k;
+        // front-facing for some direction of the bucket, and needing more than Kf for some direction of it
+        md |= (unsigned long long)(x - D[3] <= beta[q] && x + D[3] >= dthr[q]) << k;
       }
-      out[2 * ((size_t)c * nb + b)] = mf;
-      out[2 * ((size_t)c * nb + b) + 1] = md;
+      out[(size_t)c * nb + b] = md;
     }
   };
   const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
@@ -537,11 +533,39 @@ inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<u
   for (auto& x : th) x.join();
 }
 
-// The cube-map resolution of the masks: the finest of 32 / 16 / 8 / 4 / 2 cells per face edge whose masks
-// (16 bytes per cluster and bucket) fit in `budget` bytes.
+// Per cluster entry (DevScene::cl_tn): the triangle's unit normal, rounded to float, and w = 17.5 u rho rounded
+// up (danger_needs_test); w = -1 for padding and for exactly degenerate triangles with |e1||e2| <= 0.3 (never
+// pass), w = +inf for larger exactly degenerate ones (may pass for any line).
+inline void build_entry_normals(const ClusterSet& cs, std::vector<float4>& out) {
+  const int ncl = (int)cs.info.size();
+  out.assign(64 * (size_t)ncl, make_float4(0.0f, 0.0f, 0.0f, -1.0f));
+  const double u = ULP_HALF;
+  for (int c = 0; c < ncl; c++) {
+    const int2 inf = cs.info[c];
+    for (int k = 0; k < inf.y; k++) {
+      const float4 e1 = cs.ce1[inf.x + k], e2 = cs.ce2[inf.x + k];
+      const double Nx = (double)e1.y * e2.z - (double)e1.z * e2.y, Ny = (double)e1.z * e2.x - (double)e1.x * e2.z,
+                   Nz = (double)e1.x * e2.y - (double)e1.y * e2.x;
+      const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
+      const double la = std::sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
+      const double lb = std::sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+      float4& o = out[64 * (size_t)c + k];
+      if (Nl == 0.0) {
+        if (la * lb > 0.3) o.w = HUGE_VALF;
+        continue;
+      }
+      const double rho = std::max(1.0, la * lb / Nl);
+      o = make_float4((float)(Nx / Nl), (float)(Ny / Nl), (float)(Nz / Nl),
+                      std::nextafter((float)(17.5 * u * rho * (1.0 + 1e-5)), HUGE_VALF));
+    }
+  }
+}
+
+// The cube-map resolution of the masks: DIR_MASK_N cells per face edge, or the finest of 8 / 4 / 2 whose masks
+// (8 bytes per cluster and bucket) fit in `budget` bytes.
 inline int dir_mask_resolution(int ncl, size_t budget = (size_t)32 << 20) {
-  for (int n : {32, 16, 8, 4})
-    if ((size_t)ncl * 6 * n * n * 16 <= budget) return n;
+  for (int n : {DIR_MASK_N, 8, 4})
+    if ((size_t)ncl * 6 * n * n * 8 <= budget) return n;
   return 2;
 }
 

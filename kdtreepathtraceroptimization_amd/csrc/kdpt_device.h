@@ -148,10 +148,13 @@ struct DevScene {
   // g = |n . d| - cl_n.w - cull_b
   float cl_margin, cl_margin_lo, cull_a, cull_b, cull_c;
   // the exact one-level cull (kdpt_clusters.h build_dir_masks): per cluster c and direction bucket b,
-  // cl_mask[c * 6 mask_n^2 + b] = {front, danger} masks over the cluster's 64 entries; null: the fast-margin
-  // cull (tuning "cull_exact" = 0) or no one-level cull at all
-  const ulonglong2* cl_mask;
-  int mask_n;  // cube-map cells per face edge (dir_bucket)
+  // cl_mask[c * 6 mask_n^2 + b] = the danger mask over the cluster's 64 entries; null: the fast-margin cull
+  // (tuning "cull_exact" = 0) or no one-level cull at all
+  const unsigned long long* cl_mask;  // [num_clusters][6 mask_n^2] danger masks
+  int mask_n;                          // cube-map cells per face edge (dir_bucket)
+  // per cluster entry: the triangle's unit normal (float) and 17.5 u rho (the exact cull's per-triangle
+  // bound); w = -1: never passes (padding, small degenerate), w = +inf: may pass for any direction
+  const float4* cl_tn;
   const int4* snodes;
   const float4* c_v0;
   const float4* c_e1;
@@ -602,6 +605,46 @@ KDPT_HD int dir_bucket(f3 d, int n) {
   i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
   j = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
   return (face * n + j) * n + i;
+}
+
+// How far the LINE through o (direction 1 / inv, every component finite) misses the box [lo, hi], in the units
+// of cluster_may_pass's margin coefficient: the smallest K for which cluster_may_pass(lo, hi, o, inv, K) holds.
+// With the margin m = K W (W = 1 + |o - c|_1 + size_1), each slab's parameter interval [a_i, b_i] grows by
+// m |inv_i| at both ends, so the intervals meet once m >= (a_i - b_j) / (|inv_i| + |inv_j|) for every pair of
+// axes.  The line's distance from the box is at least that m (an L-infinity distance), so a point the float u/v
+// tests accept lies within K_t W of the line only if K_t >= the result.  Rounded down by 1e-5 relative; 0 when
+// the line meets the box.
+KDPT_HD float box_miss(float4 lo, float4 hi, f3 o, f3 inv) {
+  const float cx = 0.5f * (lo.x + hi.x), cy = 0.5f * (lo.y + hi.y), cz = 0.5f * (lo.z + hi.z);
+  const float W = 1.0f + fabsf(o.x - cx) + fabsf(o.y - cy) + fabsf(o.z - cz) + (hi.x - lo.x) + (hi.y - lo.y) +
+                  (hi.z - lo.z);
+  const float tlx = (lo.x - o.x) * inv.x, thx = (hi.x - o.x) * inv.x;
+  const float tly = (lo.y - o.y) * inv.y, thy = (hi.y - o.y) * inv.y;
+  const float tlz = (lo.z - o.z) * inv.z, thz = (hi.z - o.z) * inv.z;
+  const float ax = fminf(tlx, thx), bx = fmaxf(tlx, thx), ay = fminf(tly, thy), by = fmaxf(tly, thy);
+  const float az = fminf(tlz, thz), bz = fmaxf(tlz, thz);
+  const float wx = fabsf(inv.x), wy = fabsf(inv.y), wz = fabsf(inv.z);
+  const float mxy = fmaxf(ax - by, ay - bx) / (wx + wy);
+  const float mxz = fmaxf(ax - bz, az - bx) / (wx + wz);
+  const float myz = fmaxf(ay - bz, az - by) / (wy + wz);
+  const float m = fmaxf(0.0f, fmaxf(mxy, fmaxf(mxz, myz)));
+  return m / W * 0.99999f;
+}
+
+// The exact cull's per-triangle decision for a (line, cluster) pair whose line misses the cluster's box by D
+// (box_miss): may triangle tn (its float unit normal, w = 17.5 u rho, the u/v error coefficient; w < 0: never
+// passes; w = +inf: may pass for any line) pass glm's u/v tests?  Its float determinant is below -|N| (N . d -
+// beta) with beta = 5.8 u rho (1 + 1e-3) + 40 u (+ the float normal's and nd's rounding), so it cannot pass when
+// nd > beta (back-facing); otherwise a passing point lies within K_t = w / g + c (times the margin's distance
+// term) of the line, g = -nd - beta ("Cluster cull"), which needs K_t >= D, i.e. w >= (D - c) g.
+// g <= 0: no bound, the triangle is tested.
+KDPT_HD bool danger_needs_test(float4 tn, f3 d, float D, float c) {
+  if (!(tn.w >= 0.0f)) return false;
+  const float nd = tn.x * d.x + tn.y * d.y + tn.z * d.z;
+  const float beta = 0.3318f * tn.w + 3.5e-6f;
+  if (nd > beta) return false;
+  const float g = -nd - beta;
+  return !(g > 0.0f) || tn.w * 1.00001f >= (D - c) * g;
 }
 
 // The per-cluster exact margin (kdpt_clusters.h, ClusterSet::kc = {chord_eff, a, K_rig, c}) for a line of
@@ -1206,108 +1249,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   // one is tested.  Recombination by ORIGINAL index into the owner lane (order-free): last u/v pass = max
   // index, last hit = max, best = min (t, index).
   const bool big = leaf && lsize >= BIG_LEAF;
-  bool big_done = false;
-  if constexpr (!ClusterSrc::kSuper) {
-    if (S.cl_mask && __any(big)) {
-      // The exact one-level cull.  Pass: 64 (ray, cluster) pairs, lane = pair; the pair's line against the
-      // cluster's box and oriented box widened at the fast coefficient (cl_margin).  A hit selects the cluster's
-      // front mask for the ray's direction bucket, a miss its danger mask (build_dir_masks: every triangle
-      // that can pass glm's u/v tests is in the selected mask).  Then the (pair, masked triangle) items of the
-      // pass, 64 per round, lane = item, its ray from the owner's LDS slot; the results recombine on the ray's
-      // LDS slots by original index (order-free), as in the small leaves.
-      const int ncl = big ? (lsize + CLUSTER - 1) / CLUSTER : 0;
-      const int cfirst = big ? (NodeSrc::kLeafHoldsCluster ? lstart : S.leaf_cl[lnode].x) : 0;
-      const int incl = wave_incl_scan<false>(ncl);
-      const int P = __builtin_amdgcn_readlane(incl, 63);
-      const int excl = incl - ncl;
-      W->tbase[lane] = cfirst - excl;  // cluster of pair q = tbase[owner] + q
-      W->lastPass[lane] = 0ull;
-      W->lastHit[lane] = -1;
-      W->nhit[lane] = 0;
-      W->best[lane] = ~0ull;
-      wave_lds_sync();
-      if (COUNT) {
-        prof_add(WP, PROF_BIG_LEAVES, (unsigned long long)__popcll(__ballot(big)));
-        prof_add(WP, PROF_BIG_CLUSTERS, (unsigned long long)P);
-      }
-      int carry = 0;
-      for (int B = 0; B < P; B += 64) {
-        const int own = pair_owner(W->slot, excl, ncl, B, carry);
-        const int c = W->tbase[own] + B + lane;
-        const bool valid = B + lane < P;
-        unsigned long long m = valid ? ~0ull : 0ull;  // no cull: every entry (padding fails glm's determinant)
-        if (fastAABB) {
-          const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
-          const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
-          const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
-          ulonglong2 mm = make_ulonglong2(0ull, 0ull);
-          float4 clo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), chi = clo;
-          bool hit = false;
-          if (valid) {
-            mm = S.cl_mask[(size_t)c * (6 * S.mask_n * S.mask_n) + dir_bucket(dd, S.mask_n)];
-            clo = clusters.lo_of(c);
-            chi = clusters.hi_of(c);
-            hit = cluster_may_pass(clo, chi, oo, ii, S.cl_margin);
-          }
-          if (S.flat_obb && __any(hit)) {
-            if (hit) {
-              const float4 cn = S.cl_n[c];
-              hit = cluster_may_pass_obb_k(clo, chi, cn, S.cl_u[c], S.cl_v[c], S.cl_w[c], oo, ii, dd,
-                                           cn.x * dd.x + cn.y * dd.y + cn.z * dd.z, S.cl_margin);
-            }
-          }
-          m = valid ? (hit ? mm.x : mm.y) : 0ull;
-        }
-        if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
-        const int ni = __popcll(m);
-        const int iincl = wave_incl_scan<false>(ni);
-        const int Q = __builtin_amdgcn_readlane(iincl, 63);
-        const int iexcl = iincl - ni;
-        int icarry = 0;
-        for (int Rb = 0; Rb < Q; Rb += 64) {
-          if (COUNT) prof_add(WP, PROF_BIG_SWEEPS, 1);
-          const int pl = pair_owner(W->slot, iexcl, ni, Rb, icarry);
-          const int rank = Rb + lane - __builtin_amdgcn_ds_bpermute(pl << 2, iexcl);
-          const unsigned long long ml =
-              ((unsigned long long)(uint32_t)__builtin_amdgcn_ds_bpermute(pl << 2, (int)(uint32_t)(m >> 32)) << 32) |
-              (uint32_t)__builtin_amdgcn_ds_bpermute(pl << 2, (int)(uint32_t)m);
-          const int cl = __builtin_amdgcn_ds_bpermute(pl << 2, c);
-          const int rl = __builtin_amdgcn_ds_bpermute(pl << 2, own);  // the pair's ray: lane rl's
-          if (Rb + lane < Q) {
-            const int e = cl * 64 + select_bit(ml, rank);
-            const TriData T{S.c_v0[e], S.c_e1[e], S.c_e2[e]};
-            const float4 q0 = W->od[rl];
-            const float2 q1 = W->dd[rl];
-            const f3 ro = mk3(q0.x, q0.y, q0.z), rd = mk3(q0.w, q1.x, q1.y);
-            const int orig = fbits(T.e1.w);
-            float bx, by, bzk;
-            const int r = tri_test_v(T, ro, rd, bx, by, bzk);
-            if (r >= 1) atomicMax(&W->lastPass[rl], ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk));
-            if (r == 2) {
-              atomicMax(&W->lastHit[rl], orig);
-              atomicAdd(&W->nhit[rl], 1);
-              f3 hp, nn;
-              const float t = tri_hit_t<HYBRID>(S, orig, ro, rd, bx, by, bzk, hp, nn);
-              if (t > 0.0f) atomicMin(&W->best[rl], ((unsigned long long)f2u(t) << 32) | (unsigned int)orig);
-            }
-          }
-        }
-        if (COUNT) prof_lap(WP, PROF_BIG_CYC);
-      }
-      wave_lds_sync();
-      if (big) {
-        const unsigned long long lp = W->lastPass[lane];
-        r_pass = (int)(lp >> 32);
-        r_bz = u2f((uint32_t)(lp & 0xffffffffu));
-        r_lasthit = W->lastHit[lane];
-        r_nhit = W->nhit[lane];
-        r_best = W->best[lane];
-      }
-      wave_lds_sync();  // the LDS slots are rewritten by the small leaves
-      big_done = true;
-    }
-  }
-  if (!big_done && __any(big)) {
+  if (__any(big)) {
     unsigned long long k_pass = 0ull, k_best = ~0ull;
     int k_lasthit = -1, k_nhit = 0;
     // Sweeps of the (ray, cluster) pairs `pass` marks: cluster c with the ray of lane own, each surviving
@@ -1569,42 +1511,138 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       }
     } else {
       // One level: lane L owns the (ray, cluster) pairs [excl_L, excl_L + ncl_L); one pass culls 64 of them
-      // against the cluster boxes (the line misses the box: no triangle of it passes the u/v tests).
+      // against the cluster boxes (LDS) and the box survivors against the clusters' oriented boxes (L2), both
+      // widened at the fast coefficient cl_margin; the hits are swept by the whole wave.
+      // With direction masks (S.cl_mask: the exact cull, DESIGN.md 4 "Cluster cull") a miss may still hide a
+      // u/v pass of a triangle nearly parallel to the line: the cluster's danger mask for the ray's direction
+      // bucket (kdpt_clusters.h build_dir_masks) lists every triangle that can need more than cl_margin for
+      // some direction of the bucket.  Those go out as (pair, triangle) items, 64 per round; each is decided
+      // exactly from its unit normal and the pair's box_miss distance (danger_needs_test), and only the needed
+      // ones -- a handful per frame -- get glm's full test, their results recombined on the ray's LDS slots by
+      // original index (order-free) and folded into the sweeps' k_* at the end.
+      const bool exact = S.cl_mask != nullptr;
       const int cfirst = big ? (NodeSrc::kLeafHoldsCluster ? lstart : S.leaf_cl[lnode].x) : 0;
       const int incl = wave_incl_scan<false>(ncl);
       const int P = __builtin_amdgcn_readlane(incl, 63);
       const int excl = incl - ncl;
       W->tbase[lane] = cfirst - excl;  // cluster of pair q = tbase[owner] + q
+      if (exact) {
+        W->lastPass[lane] = 0ull;
+        W->lastHit[lane] = -1;
+        W->nhit[lane] = 0;
+        W->best[lane] = ~0ull;
+      }
       wave_lds_sync();
       if (COUNT) {
         prof_add(WP, PROF_BIG_LEAVES, (unsigned long long)__popcll(__ballot(big)));
         prof_add(WP, PROF_BIG_CLUSTERS, (unsigned long long)P);
       }
+      const int nbk = 6 * S.mask_n * S.mask_n;
       int carry = 0;
       for (int B = 0; B < P; B += 64) {
         const int own = pair_owner(W->slot, excl, ncl, B, carry);
         const int c = W->tbase[own] + B + lane;
-        bool pass = B + lane < P;
+        bool hit = B + lane < P;  // (no cull: every pair swept)
+        unsigned long long m = 0ull;
         if (fastAABB) {
           const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
+          const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
           float4 clo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), chi = clo;
-          if (pass) {
+          unsigned long long dm = 0ull;
+          const bool valid = hit;
+          if (valid) {
+            if (exact) dm = S.cl_mask[(size_t)c * nbk + dir_bucket(dd, S.mask_n)];
             clo = clusters.lo_of(c);
             chi = clusters.hi_of(c);
-            pass = cluster_may_pass(clo, chi, oo, ii, S.cl_margin);
+            hit = cluster_may_pass(clo, chi, oo, ii, S.cl_margin);
           }
-          // the box's survivors against the cluster's oriented box (its slabs from L2), with the margin of
-          // the second level
-          if (S.flat_obb && __any(pass)) {
-            const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
-            const CullK ck{S.cl_margin, S.cl_margin_lo, S.cull_a, S.cull_b, S.cull_c};
-            if (pass) pass = cluster_may_pass_obb(clo, chi, S.cl_n[c], S.cl_u[c], S.cl_v[c], S.cl_w[c], oo, ii, dd, ck);
+          // the box's survivors against the cluster's oriented box (its slabs from L2)
+          if (S.flat_obb && __any(hit)) {
+            if (hit) {
+              const float4 cn = S.cl_n[c];
+              hit = cluster_may_pass_obb_k(clo, chi, cn, S.cl_u[c], S.cl_v[c], S.cl_w[c], oo, ii, dd,
+                                           cn.x * dd.x + cn.y * dd.y + cn.z * dd.z, S.cl_margin);
+            }
+          }
+          if (exact) m = (valid && !hit) ? dm : 0ull;
+        }
+        if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
+        sweep(hit, c, own);
+        if (COUNT) prof_lap(WP, PROF_BIG_CYC);
+        if (!exact || !__any(m != 0ull)) continue;
+        // (the line, its direction and its distance from the box, recomputed rather than kept across the sweep)
+        const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
+        float D = 0.0f;
+        {
+          const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
+          const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
+          if (m) D = box_miss(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
+        }
+        // the missed pairs' danger triangles: lane = item (owner pair from pair_owner, entry from its mask), the
+        // next round's normal records fetched while this round is decided
+        const int ni = __popcll(m);
+        const int iincl = wave_incl_scan<false>(ni);
+        const int Q = __builtin_amdgcn_readlane(iincl, 63);
+        const int iexcl = iincl - ni;
+        int icarry = 0;
+        auto item = [&](int Rb, int& pl, int& e) {
+          pl = pair_owner(W->slot, iexcl, ni, Rb, icarry);
+          const int rank = Rb + lane - __builtin_amdgcn_ds_bpermute(pl << 2, iexcl);
+          const unsigned long long ml =
+              ((unsigned long long)(uint32_t)__builtin_amdgcn_ds_bpermute(pl << 2, (int)(uint32_t)(m >> 32)) << 32) |
+              (uint32_t)__builtin_amdgcn_ds_bpermute(pl << 2, (int)(uint32_t)m);
+          const bool v = Rb + lane < Q;
+          e = v ? __builtin_amdgcn_ds_bpermute(pl << 2, c) * 64 + select_bit(ml, rank) : -1;
+          return v;
+        };
+        int ipl = 0, ie = -1;
+        bool iv = Q > 0 && item(0, ipl, ie);
+        float4 tn = iv ? S.cl_tn[ie] : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+        for (int Rb = 0; Rb < Q; Rb += 64) {
+          const int cpl = ipl, ce = ie;
+          const float4 ct = tn;
+          const bool cv = iv;
+          if (Rb + 64 < Q) {
+            iv = item(Rb + 64, ipl, ie);
+            tn = iv ? S.cl_tn[ie] : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
+          }
+          const f3 rd = mk3(bpermute_f(dd.x, cpl), bpermute_f(dd.y, cpl), bpermute_f(dd.z, cpl));
+          const float rD = bpermute_f(D, cpl);
+          const bool need = cv && danger_needs_test(ct, rd, rD, S.cull_c);
+          if (COUNT) prof_add(WP, PROF_BIG_SWEEPS, 1);
+          if (__any(need)) {
+            if (COUNT) prof_add(WP, PROF_BIG_PASS, 1);
+            const int rl = __builtin_amdgcn_ds_bpermute(cpl << 2, own);  // the pair's ray: lane rl's
+            const f3 ro = mk3(bpermute_f(o.x, rl), bpermute_f(o.y, rl), bpermute_f(o.z, rl));
+            if (need) {
+              const TriData T{S.c_v0[ce], S.c_e1[ce], S.c_e2[ce]};
+              const int orig = fbits(T.e1.w);
+              float bx, by, bzk;
+              const int r = tri_test_v(T, ro, rd, bx, by, bzk);
+              if (r >= 1) atomicMax(&W->lastPass[rl], ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk));
+              if (r == 2) {
+                atomicMax(&W->lastHit[rl], orig);
+                atomicAdd(&W->nhit[rl], 1);
+                f3 hp, nn;
+                const float t = tri_hit_t<HYBRID>(S, orig, ro, rd, bx, by, bzk, hp, nn);
+                if (t > 0.0f) atomicMin(&W->best[rl], ((unsigned long long)f2u(t) << 32) | (unsigned int)orig);
+              }
+            }
           }
         }
         if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
-        sweep(pass, c, own);
-        if (COUNT) prof_lap(WP, PROF_BIG_CYC);
+      }
+      if (exact) {
+        wave_lds_sync();
+        if (big) {  // the danger triangles' results folded into the sweeps'
+          const unsigned long long lp = W->lastPass[lane], lb = W->best[lane];
+          k_pass = lp > k_pass ? lp : k_pass;
+          k_lasthit = max(k_lasthit, W->lastHit[lane]);
+          k_nhit += W->nhit[lane];
+          k_best = lb < k_best ? lb : k_best;
+        }
+        wave_lds_sync();  // the LDS slots are rewritten by the small leaves
       }
     }
     if (big) {

@@ -1694,7 +1694,8 @@ struct kdpt_ctx {
   CullMargin cull{};                // the scene's cluster-cull margins (kdpt_clusters.h cluster_margin)
   // the exact one-level cull's direction masks (kdpt_clusters.h build_dir_masks), built when the scene's rigorous
   // margin is above the cap; S.cl_mask points at them unless a knob chose another cull
-  ulonglong2* mask_dev = nullptr;
+  unsigned long long* mask_dev = nullptr;
+  float4* tn_dev = nullptr;  // the clusters' per-entry normal records (DevScene::cl_tn)
   int mask_n = 0;
   bool cull_exact = true;   // "cull_exact" knob: 0 = the fast-margin cull (not exact for such scenes)
   bool cull_scene = true;   // false after "cluster_cull" = 0 or a fixed "cull_margin"
@@ -1978,14 +1979,20 @@ void fix_cull(kdpt_ctx* c, float K) {
 void apply_cull_route(kdpt_ctx* c) {
   c->S.cl_mask = (c->mask_dev && c->cull_exact && c->cull_scene) ? c->mask_dev : nullptr;
   c->S.mask_n = c->mask_n;
+  c->S.cl_tn = c->tn_dev;
 }
 // The direction masks of the scene's clusters at resolution n (cube-map cells per face edge), uploaded.
 int build_masks(kdpt_ctx* c, int n) {
   std::vector<unsigned long long> m;
   build_dir_masks(*c->mask_cs, n, c->cull.K, m);
-  ulonglong2* d = nullptr;
-  int rc = dupload(c, &d, reinterpret_cast<const ulonglong2*>(m.data()), m.size() / 2);
+  unsigned long long* d = nullptr;
+  int rc = dupload(c, &d, m.data(), m.size());
   if (rc) return rc;
+  if (!c->tn_dev) {
+    std::vector<float4> tn;
+    build_entry_normals(*c->mask_cs, tn);
+    if ((rc = dupload(c, &c->tn_dev, tn.data(), tn.size()))) return rc;
+  }
   c->mask_dev = d;
   c->mask_n = n;
   apply_cull_route(c);
@@ -2684,7 +2691,7 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
       // 0: the fast-margin one-level cull instead of the masked exact one (A/B; not exact for such scenes)
       c->cull_exact = v != 0;
     } else {
-      if (v != 2 && v != 4 && v != 8 && v != 16 && v != 32) return fail(KDPT_ERR_ARG, "cull_mask_n must be 2, 4, 8, 16 or 32");
+      if (v < 1 || v > 128) return fail(KDPT_ERR_ARG, "cull_mask_n must be in 1 .. 128");
       if (!c->mask_cs) return fail(KDPT_ERR_ARG, "cull_mask_n: this scene has no direction masks");
       int rc = build_masks(c, v);
       if (rc) return rc;

@@ -31,7 +31,7 @@ struct Counts {
   long long lines = 0, pass = 0;           // lines tested, (line, cluster) pairs with a u/v pass
   long long culled_box = 0, viol_box = 0;  // one-level cull (dragon_5's LDS route)
   long long viol_slab = 0, viol_super = 0, viol_chunk = 0, viol_obb = 0;
-  long long viol_mask = 0, mask_items = 0;  // the exact one-level cull (build_dir_masks)
+  long long viol_mask = 0, mask_items = 0, mask_needed = 0;  // the exact one-level cull (build_dir_masks)
   long long nofast = 0;                    // some invdir component infinite: the wave does not cull
   long long margin_used = 0;               // passing pairs the box cull passes only thanks to the margin
   // over the passing (line, triangle) pairs: the largest distance of the line's exact crossing of the
@@ -41,7 +41,7 @@ struct Counts {
   void add(const Counts& o) {
     lines += o.lines; pass += o.pass; culled_box += o.culled_box; viol_box += o.viol_box;
     viol_slab += o.viol_slab; viol_super += o.viol_super; viol_chunk += o.viol_chunk; viol_obb += o.viol_obb;
-    viol_mask += o.viol_mask; mask_items += o.mask_items;
+    viol_mask += o.viol_mask; mask_items += o.mask_items; mask_needed += o.mask_needed;
     nofast += o.nofast; margin_used += o.margin_used; worst = std::max(worst, o.worst);
     bound = std::max(bound, o.bound);
   }
@@ -221,11 +221,16 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
   long long leaves = 0, pairs = 0, old_sw = 0, new_sw = 0, prod = 0, back = 0, front = 0, graze = 0, viol_old = 0,
             viol_new = 0, nofast = 0, small_tris = 0, old_tris = 0, new_tris = 0, graze_tris = 0, ref_susp = 0,
             ref_items = 0, ref_back = 0, ref_sw = 0, ref_tris = 0, refq_sw = 0, viol_ref = 0, cmp_rounds = 0,
-            cmp_items = 0, viol_cmp = 0, msk_items = 0, msk_pairs = 0, viol_msk = 0;
-  const int mask_n = getenv("MASK_N") ? atoi(getenv("MASK_N")) : 16;
-  std::vector<unsigned long long> masks;
+            cmp_items = 0, viol_cmp = 0, msk_items = 0, msk_pairs = 0, viol_msk = 0, msk_needed = 0, t2_near = 0,
+            t2_items = 0, viol_t2 = 0;
+  const int mask_n = getenv("MASK_N") ? atoi(getenv("MASK_N")) : DIR_MASK_N;
+  const float KD = getenv("MASK_KD") ? (float)atof(getenv("MASK_KD")) : 1e-3f;
+  std::vector<unsigned long long> masks, masks2;
   build_dir_masks(cs, mask_n, CULL_MARGIN_FAST, masks);
-#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, pairs, old_sw, new_sw, prod, back, front, graze, viol_old, viol_new, nofast, small_tris, old_tris, new_tris, graze_tris, ref_susp, ref_items, ref_back, ref_sw, ref_tris, refq_sw, viol_ref, cmp_rounds, cmp_items, viol_cmp, msk_items, msk_pairs, viol_msk)
+  build_dir_masks(cs, mask_n, KD, masks2);
+  std::vector<float4> tn;
+  build_entry_normals(cs, tn);
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, pairs, old_sw, new_sw, prod, back, front, graze, viol_old, viol_new, nofast, small_tris, old_tris, new_tris, graze_tris, ref_susp, ref_items, ref_back, ref_sw, ref_tris, refq_sw, viol_ref, cmp_rounds, cmp_items, viol_cmp, msk_items, msk_pairs, viol_msk, msk_needed, t2_near, t2_items, viol_t2)
   for (long long i = 0; i < nr; i++) {
     const f3 o = mk3(r[6 * i], r[6 * i + 1], r[6 * i + 2]), d = mk3(r[6 * i + 3], r[6 * i + 4], r[6 * i + 5]);
     const f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -351,16 +356,35 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
               viol_cmp += pass;
             }
           }
-          // the bucket-mask design (build_dir_masks): the pair tests its front or danger triangles
-          {
+          // two tiers (experiment): pairs that also miss the boxes widened at KD use masks built for KD
+          if (!fast_ok) {
+            const bool nearp = cluster_may_pass(L, H, o, inv, KD) &&
+                               cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, KD);
             const int bk = dir_bucket(d, mask_n);
-            const unsigned long long mk = masks[2 * ((size_t)c * 6 * mask_n * mask_n + bk) + (fast_ok ? 0 : 1)];
-            msk_items += __builtin_popcountll(mk);
-            msk_pairs += mk != 0ull;
+            const unsigned long long mk = nearp ? masks[(size_t)c * 6 * mask_n * mask_n + bk]
+                                                : masks2[(size_t)c * 6 * mask_n * mask_n + bk];
+            t2_near += nearp;
+            t2_items += __builtin_popcountll(mk);
             for (int k = 0; k < inf.y; k++) {
               float bx, by, bz;
               const bool p1 = tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, o, d, bx, by, bz) >= 1;
-              viol_msk += p1 && !((mk >> k) & 1ull);
+              viol_t2 += p1 && !((mk >> k) & 1ull);
+            }
+          }
+          // the product's exact cull: a fast-box hit is swept; a miss walks its danger mask and tests the
+          // triangles danger_needs_test keeps
+          if (!fast_ok) {
+            const int bk = dir_bucket(d, mask_n);
+            const unsigned long long mk = masks[(size_t)c * 6 * mask_n * mask_n + bk];
+            const float Dm = box_miss(L, H, o, inv);
+            msk_items += __builtin_popcountll(mk);
+            msk_pairs += mk != 0ull;
+            for (int k = 0; k < inf.y; k++) {
+              const bool need = ((mk >> k) & 1ull) && danger_needs_test(tn[64 * (size_t)c + k], d, Dm, cm.c);
+              msk_needed += need;
+              float bx, by, bz;
+              const bool p1 = tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, o, d, bx, by, bz) >= 1;
+              viol_msk += p1 && !need;
             }
           }
           ref_sw += ok;
@@ -385,11 +409,13 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
          "\"viol_new\": %lld, \"nofast\": %lld, \"small_tris\": %.3f, \"old_tris\": %.3f, \"new_tris\": %.3f, "
          "\"graze_tris\": %.3f, \"ref_susp\": %.4f, \"ref_items\": %.3f, \"ref_back\": %.4f, \"ref_sweeps\": %.4f, "
          "\"ref_tris\": %.3f, \"refq_sweeps\": %.4f, \"viol_ref\": %lld, \"cmp_rounds\": %.4f, \"cmp_items\": %.3f, "
-         "\"viol_cmp\": %lld, \"mask_n\": %d, \"msk_items\": %.3f, \"msk_pairs\": %.4f, \"viol_msk\": %lld}\n",
+         "\"viol_cmp\": %lld, \"mask_n\": %d, \"msk_items\": %.3f, \"msk_pairs\": %.4f, \"viol_msk\": %lld, "
+         "\"msk_needed\": %.4f, \"t2_near\": %.4f, \"t2_items\": %.3f, \"viol_t2\": %lld}\n",
          nr, cs.info.size(), grp.mode, grp.chord, leaves / R, pairs / R, old_sw / R, new_sw / R, prod / R, back / R,
          front / R, graze / R, viol_old, viol_new, nofast, small_tris / R, old_tris / R, new_tris / R, graze_tris / R,
          ref_susp / R, ref_items / R, ref_back / R, ref_sw / R, ref_tris / R, refq_sw / R, viol_ref, cmp_rounds / R,
-         cmp_items / R, viol_cmp, mask_n, msk_items / R, msk_pairs / R, viol_msk);
+         cmp_items / R, viol_cmp, mask_n, msk_items / R, msk_pairs / R, viol_msk, msk_needed / R, t2_near / R,
+         t2_items / R, viol_t2);
   return 0;
 }
 
@@ -460,6 +486,8 @@ int main(int argc, char** argv) {
   const int mask_n = getenv("MASK_N") ? atoi(getenv("MASK_N")) : DIR_MASK_N;
   std::vector<unsigned long long> masks;
   build_dir_masks(cs, mask_n, CULL_MARGIN_FAST, masks);
+  std::vector<float4> tn;
+  build_entry_normals(cs, tn);
   Counts tot[NGEN];
   const int nthreads = 1;
 #pragma omp parallel
@@ -604,20 +632,26 @@ int main(int argc, char** argv) {
       }
       const bool box = cluster_may_pass(L, H, of, inv, K);
       if (!box) C.culled_box++;
-      {
-        // the exact one-level cull: the cluster's front mask when the line hits the Kf-widened box and
-        // oriented box, else its danger mask; every triangle passing glm's u/v tests must be in it
+      if (fast) {
+        // the exact one-level cull: a line that misses the cluster's fast-margin box and oriented box tests only
+        // the triangles of the cluster's danger mask that danger_needs_test keeps; every triangle passing glm's
+        // u/v tests must be among them
         const float ndv = cs.nrm[c].x * df.x + cs.nrm[c].y * df.y + cs.nrm[c].z * df.z;
         const bool hit = cluster_may_pass(L, H, of, inv, CULL_MARGIN_FAST) &&
                          cluster_may_pass_obb_k(L, H, cs.nrm[c], cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], of, inv, df, ndv,
                                                 CULL_MARGIN_FAST);
-        const unsigned long long mk = masks[2 * ((size_t)c * 6 * mask_n * mask_n + dir_bucket(df, mask_n)) + (hit ? 0 : 1)];
-        C.mask_items += __builtin_popcountll(mk);
-        for (int k = 0; k < inf.y; k++) {
-          float bx, by, bz;
-          if (tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, of, df, bx, by, bz) >= 1 &&
-              !((mk >> k) & 1ull))
-            C.viol_mask++;
+        if (!hit) {
+          const unsigned long long mk = masks[(size_t)c * 6 * mask_n * mask_n + dir_bucket(df, mask_n)];
+          const float Dm = box_miss(L, H, of, inv);
+          C.mask_items += __builtin_popcountll(mk);
+          for (int k = 0; k < inf.y; k++) {
+            const bool need = ((mk >> k) & 1ull) && danger_needs_test(tn[64 * (size_t)c + k], df, Dm, cm.c);
+            C.mask_needed += need;
+            float bx, by, bz;
+            if (tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, of, df, bx, by, bz) >= 1 &&
+                !need)
+              C.viol_mask++;
+          }
         }
       }
       if (pass) {
@@ -654,9 +688,10 @@ int main(int argc, char** argv) {
     all.add(C);
     printf("%s\"%s\": {\"lines\": %lld, \"pass\": %lld, \"culled_box\": %lld, \"viol_box\": %lld, \"viol_slab\": %lld, "
            "\"viol_super\": %lld, \"viol_chunk\": %lld, \"viol_obb\": %lld, \"viol_mask\": %lld, \"mask_items\": %lld, "
+           "\"mask_needed\": %lld, "
            "\"nofast\": %lld, \"margin_used\": %lld, \"worst\": %.4g, \"bound\": %.4g}",
            g ? ", " : "", kGenName[g], C.lines, C.pass, C.culled_box, C.viol_box, C.viol_slab, C.viol_super,
-           C.viol_chunk, C.viol_obb, C.viol_mask, C.mask_items, C.nofast, C.margin_used, C.worst, C.bound);
+           C.viol_chunk, C.viol_obb, C.viol_mask, C.mask_items, C.mask_needed, C.nofast, C.margin_used, C.worst, C.bound);
   }
   printf("}, \"violations\": %lld, \"viol_mask\": %lld, \"lines\": %lld, \"pass\": %lld, \"margin_used\": %lld, "
          "\"worst\": %.4g, \"bound\": %.4g}\n",
