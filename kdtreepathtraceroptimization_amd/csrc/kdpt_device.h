@@ -155,6 +155,12 @@ struct DevScene {
   // per cluster entry: the triangle's unit normal (float) and 17.5 u rho (the exact cull's per-triangle
   // bound); w = -1: never passes (padding, small degenerate), w = +inf: may pass for any direction
   const float4* cl_tn;
+  // the production intersect kernel's record of the (ray, cluster) pairs whose line missed the fast-margin
+  // boxes (exact cull): rec[i] = {ray id (iteration << 24 | queue slot), cluster}, rec_n = their number
+  // (rec_cap at most: beyond it the kernel stops recording and k_fixup re-traces the whole launch)
+  int2* rec;
+  int* rec_n;
+  int rec_cap;
   const int4* snodes;
   const float4* c_v0;
   const float4* c_e1;
@@ -279,6 +285,7 @@ struct Hit {
   f3 ip, normal;
   bool obj_intersect;
   int objMaterialIdx;
+  int tri;  // traverseKD: the triangle whose hit won (valid when obj_intersect)
 };
 
 struct TraverseCounters {
@@ -413,6 +420,7 @@ KDPT_HD void traverseKD(const DevScene& S, const Ray& ray, Hit& h, int material_
           h.ip = hit;
           h.normal = norm;
           h.obj_intersect = true;
+          h.tri = i;
         }
       }
     }
@@ -871,6 +879,7 @@ struct WaveLeafLDS {
   int lastHit[64];
   int nhit[64];
   unsigned long long best[64];  // (t bits << 32) | triangle index, min
+  int rid[64];     // the lane's ray id for the exact cull's records (iteration << 24 | queue slot)
 };
 
 // Count mode only (the counting intersect kernel allocates one per wave, the others one unused record, so
@@ -1516,17 +1525,20 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       // With direction masks (S.cl_mask: the exact cull, DESIGN.md 4 "Cluster cull") a miss may still hide a
       // u/v pass of a triangle nearly parallel to the line: the cluster's danger mask for the ray's direction
       // bucket (kdpt_clusters.h build_dir_masks) lists every triangle that can need more than cl_margin for
-      // some direction of the bucket.  Those go out as (pair, triangle) items, 64 per round; each is decided
-      // exactly from its unit normal and the pair's box_miss distance (danger_needs_test), and only the needed
-      // ones -- a handful per frame -- get glm's full test, their results recombined on the ray's LDS slots by
-      // original index (order-free) and folded into the sweeps' k_* at the end.
+      // some direction of the bucket.  The production kernel records the missed pairs and goes on (k_fixup
+      // decides them after the launch and re-traces the rare ray that needed one).  The counting kernel
+      // decides them here, so that its counters are the exact walk's: the danger triangles go out as (pair,
+      // triangle) items, 64 per round; each is decided from its unit normal and the pair's box_miss distance
+      // (danger_needs_test), and only the needed ones -- a handful per frame -- get glm's full test, their
+      // results recombined on the ray's LDS slots by original index (order-free) and folded into the sweeps'
+      // k_* at the end.
       const bool exact = S.cl_mask != nullptr;
       const int cfirst = big ? (NodeSrc::kLeafHoldsCluster ? lstart : S.leaf_cl[lnode].x) : 0;
       const int incl = wave_incl_scan<false>(ncl);
       const int P = __builtin_amdgcn_readlane(incl, 63);
       const int excl = incl - ncl;
       W->tbase[lane] = cfirst - excl;  // cluster of pair q = tbase[owner] + q
-      if (exact) {
+      if (COUNT && exact) {
         W->lastPass[lane] = 0ull;
         W->lastHit[lane] = -1;
         W->nhit[lane] = 0;
@@ -1552,7 +1564,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
           unsigned long long dm = 0ull;
           const bool valid = hit;
           if (valid) {
-            if (exact) dm = S.cl_mask[(size_t)c * nbk + dir_bucket(dd, S.mask_n)];
+            if (exact && COUNT) dm = S.cl_mask[(size_t)c * nbk + dir_bucket(dd, S.mask_n)];
             clo = clusters.lo_of(c);
             chi = clusters.hi_of(c);
             hit = cluster_may_pass(clo, chi, oo, ii, S.cl_margin);
@@ -1565,12 +1577,30 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
                                            cn.x * dd.x + cn.y * dd.y + cn.z * dd.z, S.cl_margin);
             }
           }
-          if (exact) m = (valid && !hit) ? dm : 0ull;
+          // (the production kernel records every missed pair; k_fixup reads its danger mask)
+          if (exact) m = (valid && !hit) ? (COUNT ? dm : 1ull) : 0ull;
         }
         if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
         sweep(hit, c, own);
         if (COUNT) prof_lap(WP, PROF_BIG_CYC);
-        if (!exact || !__any(m != 0ull)) continue;
+        if (!exact) continue;
+        if (!COUNT) {
+          // Production kernel: speculate.  The traversal goes on as if no danger triangle passed (almost always
+          // so); the missed pairs are recorded, and k_fixup decides them after the launch -- any that hides a
+          // u/v pass gets its ray re-traced exactly (traverseKD), which replaces its hit record.  (The counting
+          // kernel decides them here instead, so that its counters are the exact traversal's.)
+          const bool rc = m != 0ull;
+          const unsigned long long rm = __ballot(rc);
+          if (rm) {
+            int base = 0;
+            if (lane == 0) base = atomicAdd(S.rec_n, __popcll(rm));
+            base = __builtin_amdgcn_readfirstlane(base);
+            const int slot = base + (int)lane_prefix(rm);
+            if (rc && slot < S.rec_cap) S.rec[slot] = make_int2(W->rid[own], c);
+          }
+          continue;
+        }
+        if (!__any(m != 0ull)) continue;
         // (the line, its direction and its distance from the box, recomputed rather than kept across the sweep)
         const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
         float D = 0.0f;
@@ -1633,7 +1663,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         }
         if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
       }
-      if (exact) {
+      if (COUNT && exact) {
         wave_lds_sync();
         if (big) {  // the danger triangles' results folded into the sweeps'
           const unsigned long long lp = W->lastPass[lane], lb = W->best[lane];
