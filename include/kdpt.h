@@ -178,11 +178,6 @@ typedef struct kdpt_stats {
                                     kdpt_trace_iterations (1 for one-at-a-time tracing) */
     long long total_trace_rays;  /* since create/reset: rays handed to the KD traversal kernel (k_trace), i.e.
                                     the segments whose ray meets the KD root box */
-    long long cull_records_total;  /* since create/reset: (ray, cluster) pairs the exact cull's production
-                                      kernel left for k_fixup (rays whose line missed a cluster's fast-margin
-                                      box in a big leaf) */
-    long long cull_retraces_total; /* ... and the rays k_fixup traced again (a danger triangle passed glm's
-                                      u/v tests; every ray of a launch whose records overflowed) */
 } kdpt_stats;
 
 typedef struct kdpt_ctx kdpt_ctx;

@@ -453,7 +453,7 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
 // lies on the face plane at |y| >= R, where radial projection is (1/R)-Lipschitz, so r_b = half diagonal / R.
 // So |N . d - N . d_b| <= r_b (+ 1e-6 for the float d's length).  Exactly degenerate triangles are in every mask
 // when |e1||e2| > 0.3 and in none otherwise (their float determinant stays below FLT_EPSILON).
-constexpr int DIR_MASK_N = 32;  // default cube-map cells per face edge (6 n^2 buckets)
+constexpr int DIR_MASK_N = 128;  // finest cube-map cells per face edge (6 n^2 buckets; dir_mask_resolution)
 inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<unsigned long long>& out) {
   const int ncl = (int)cs.info.size(), nb = 6 * n * n;
   out.assign((size_t)nb * ncl, 0ull);
@@ -561,10 +561,13 @@ inline void build_entry_normals(const ClusterSet& cs, std::vector<float4>& out) 
   }
 }
 
-// The cube-map resolution of the masks: DIR_MASK_N cells per face edge, or the finest of 8 / 4 / 2 whose masks
-// (8 bytes per cluster and bucket) fit in `budget` bytes.
-inline int dir_mask_resolution(int ncl, size_t budget = (size_t)32 << 20) {
-  for (int n : {DIR_MASK_N, 8, 4})
+// The cube-map resolution of the masks: the finest of DIR_MASK_N, 64, 32, ... 4 cells per face edge whose masks
+// (8 bytes per cluster and bucket) fit in `budget` bytes, else 2.  A danger mask holds the triangles whose plane
+// passes within the bucket's radius (plus a band of 17.5 u rho / (Kf - c)) of its directions, so its bit count
+// falls with the bucket size: on C3 (dragon_5, 181 clusters, 142 MB at 128) the masked cull measured 0.80 of the
+// fast-margin cull's rate at 32 cells and Kf = 1e-4, 0.88 at 128 cells and Kf = 1e-3 (profiles/r05_ab_log.md).
+inline int dir_mask_resolution(int ncl, size_t budget = (size_t)160 << 20) {
+  for (int n : {DIR_MASK_N, 64, 32, 16, 8, 4})
     if ((size_t)ncl * 6 * n * n * 8 <= budget) return n;
   return 2;
 }
@@ -618,7 +621,10 @@ struct CullMargin {
   double rigorous;  // K_rigorous for these triangles
   bool exact;       // K >= K_rigorous: the cull never drops a triangle that passes glm's u/v tests
 };
-constexpr float CULL_MARGIN_FAST = 1e-4f;  // the margin of meshes whose K_rigorous exceeds the cap
+constexpr float CULL_MARGIN_FAST = 1e-4f;  // the slab level's floor (K_lo)
+// the box coefficient of meshes whose K_rigorous exceeds the cap (their masked cull): 10x the floor narrows the
+// danger band of their direction masks tenfold and costs no measurable sweeps (profiles/r05_ab_log.md)
+constexpr float CULL_MARGIN_MASKED = 1e-3f;
 constexpr double CULL_MARGIN_CAP = 2e-3;   // largest K_rigorous worth using (beyond it the cull loses its bite)
 inline CullMargin cluster_margin(const std::vector<float4>& v0, const std::vector<float4>& e1,
                                  const std::vector<float4>& e2) {
@@ -639,7 +645,7 @@ inline CullMargin cluster_margin(const std::vector<float4>& v0, const std::vecto
   r.rigorous = 8.75 * pmax + 64.0 * u * (1.0 + cmax + emax);
   r.exact = r.rigorous <= CULL_MARGIN_CAP;
   r.K_lo = CULL_MARGIN_FAST;
-  r.K = r.exact ? std::max(std::nextafter((float)r.rigorous, FLT_MAX), CULL_MARGIN_FAST) : CULL_MARGIN_FAST;
+  r.K = r.exact ? std::max(std::nextafter((float)r.rigorous, FLT_MAX), CULL_MARGIN_FAST) : CULL_MARGIN_MASKED;
   r.a = std::nextafter((float)(17.5 * u * rho * (1.0 + 1e-5)), FLT_MAX);
   r.b = std::nextafter((float)(5.8 * u * rho + 10.0 * u), FLT_MAX);
   r.c = std::nextafter((float)(64.0 * u * (1.0 + cmax + emax)), FLT_MAX);

@@ -148,19 +148,14 @@ struct DevScene {
   // g = |n . d| - cl_n.w - cull_b
   float cl_margin, cl_margin_lo, cull_a, cull_b, cull_c;
   // the exact one-level cull (kdpt_clusters.h build_dir_masks): per cluster c and direction bucket b,
-  // cl_mask[c * 6 mask_n^2 + b] = the danger mask over the cluster's 64 entries; null: the fast-margin cull
+  // cl_mask[b * num_clusters + c] = the danger mask over the cluster's 64 entries (bucket-major: a ray's
+  // pairs, consecutive clusters of one leaf in one bucket, share cache lines); null: the fast-margin cull
   // (tuning "cull_exact" = 0) or no one-level cull at all
   const unsigned long long* cl_mask;  // [num_clusters][6 mask_n^2] danger masks
   int mask_n;                          // cube-map cells per face edge (dir_bucket)
   // per cluster entry: the triangle's unit normal (float) and 17.5 u rho (the exact cull's per-triangle
   // bound); w = -1: never passes (padding, small degenerate), w = +inf: may pass for any direction
   const float4* cl_tn;
-  // the production intersect kernel's record of the (ray, cluster) pairs whose line missed the fast-margin
-  // boxes (exact cull): rec[i] = {ray id (iteration << 24 | queue slot), cluster}, rec_n = their number
-  // (rec_cap at most: beyond it the kernel stops recording and k_fixup re-traces the whole launch)
-  int2* rec;
-  int* rec_n;
-  int rec_cap;
   const int4* snodes;
   const float4* c_v0;
   const float4* c_e1;
@@ -285,7 +280,6 @@ struct Hit {
   f3 ip, normal;
   bool obj_intersect;
   int objMaterialIdx;
-  int tri;  // traverseKD: the triangle whose hit won (valid when obj_intersect)
 };
 
 struct TraverseCounters {
@@ -420,7 +414,6 @@ KDPT_HD void traverseKD(const DevScene& S, const Ray& ray, Hit& h, int material_
           h.ip = hit;
           h.normal = norm;
           h.obj_intersect = true;
-          h.tri = i;
         }
       }
     }
@@ -879,7 +872,6 @@ struct WaveLeafLDS {
   int lastHit[64];
   int nhit[64];
   unsigned long long best[64];  // (t bits << 32) | triangle index, min
-  int rid[64];     // the lane's ray id for the exact cull's records (iteration << 24 | queue slot)
 };
 
 // Count mode only (the counting intersect kernel allocates one per wave, the others one unused record, so
@@ -1525,37 +1517,26 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       // With direction masks (S.cl_mask: the exact cull, DESIGN.md 4 "Cluster cull") a miss may still hide a
       // u/v pass of a triangle nearly parallel to the line: the cluster's danger mask for the ray's direction
       // bucket (kdpt_clusters.h build_dir_masks) lists every triangle that can need more than cl_margin for
-      // some direction of the bucket.  The production kernel records the missed pairs and goes on (k_fixup
-      // decides them after the launch and re-traces the rare ray that needed one).  The counting kernel
-      // decides them here, so that its counters are the exact walk's: the danger triangles go out as (pair,
-      // triangle) items, 64 per round; each is decided from its unit normal and the pair's box_miss distance
-      // (danger_needs_test), and only the needed ones -- a handful per frame -- get glm's full test, their
-      // results recombined on the ray's LDS slots by original index (order-free) and folded into the sweeps'
-      // k_* at the end.
+      // some direction of the bucket.  The missed pair's lane walks those bits itself: each triangle is
+      // decided from its unit normal and the line's box_miss distance (danger_needs_test), and the rare one
+      // that needs it gets glm's u/v tests; a pass turns the miss into a hit, so the whole cluster is swept
+      // like the uncull'd walk would.  (A superset of the clusters with a u/v pass is swept: exact.)
       const bool exact = S.cl_mask != nullptr;
       const int cfirst = big ? (NodeSrc::kLeafHoldsCluster ? lstart : S.leaf_cl[lnode].x) : 0;
       const int incl = wave_incl_scan<false>(ncl);
       const int P = __builtin_amdgcn_readlane(incl, 63);
       const int excl = incl - ncl;
       W->tbase[lane] = cfirst - excl;  // cluster of pair q = tbase[owner] + q
-      if (COUNT && exact) {
-        W->lastPass[lane] = 0ull;
-        W->lastHit[lane] = -1;
-        W->nhit[lane] = 0;
-        W->best[lane] = ~0ull;
-      }
       wave_lds_sync();
       if (COUNT) {
         prof_add(WP, PROF_BIG_LEAVES, (unsigned long long)__popcll(__ballot(big)));
         prof_add(WP, PROF_BIG_CLUSTERS, (unsigned long long)P);
       }
-      const int nbk = 6 * S.mask_n * S.mask_n;
       int carry = 0;
       for (int B = 0; B < P; B += 64) {
         const int own = pair_owner(W->slot, excl, ncl, B, carry);
         const int c = W->tbase[own] + B + lane;
         bool hit = B + lane < P;  // (no cull: every pair swept)
-        unsigned long long m = 0ull;
         if (fastAABB) {
           const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
@@ -1564,7 +1545,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
           unsigned long long dm = 0ull;
           const bool valid = hit;
           if (valid) {
-            if (exact && COUNT) dm = S.cl_mask[(size_t)c * nbk + dir_bucket(dd, S.mask_n)];
+            if (exact) dm = S.cl_mask[(size_t)dir_bucket(dd, S.mask_n) * S.num_clusters + c];
             clo = clusters.lo_of(c);
             chi = clusters.hi_of(c);
             hit = cluster_may_pass(clo, chi, oo, ii, S.cl_margin);
@@ -1577,102 +1558,35 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
                                            cn.x * dd.x + cn.y * dd.y + cn.z * dd.z, S.cl_margin);
             }
           }
-          // (the production kernel records every missed pair; k_fixup reads its danger mask)
-          if (exact) m = (valid && !hit) ? (COUNT ? dm : 1ull) : 0ull;
-        }
-        if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
-        sweep(hit, c, own);
-        if (COUNT) prof_lap(WP, PROF_BIG_CYC);
-        if (!exact) continue;
-        if (!COUNT) {
-          // Production kernel: speculate.  The traversal goes on as if no danger triangle passed (almost always
-          // so); the missed pairs are recorded, and k_fixup decides them after the launch -- any that hides a
-          // u/v pass gets its ray re-traced exactly (traverseKD), which replaces its hit record.  (The counting
-          // kernel decides them here instead, so that its counters are the exact traversal's.)
-          const bool rc = m != 0ull;
-          const unsigned long long rm = __ballot(rc);
-          if (rm) {
-            int base = 0;
-            if (lane == 0) base = atomicAdd(S.rec_n, __popcll(rm));
-            base = __builtin_amdgcn_readfirstlane(base);
-            const int slot = base + (int)lane_prefix(rm);
-            if (rc && slot < S.rec_cap) S.rec[slot] = make_int2(W->rid[own], c);
-          }
-          continue;
-        }
-        if (!__any(m != 0ull)) continue;
-        // (the line, its direction and its distance from the box, recomputed rather than kept across the sweep)
-        const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
-        float D = 0.0f;
-        {
-          const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
-          const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
-          if (m) D = box_miss(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
-        }
-        // the missed pairs' danger triangles: lane = item (owner pair from pair_owner, entry from its mask), the
-        // next round's normal records fetched while this round is decided
-        const int ni = __popcll(m);
-        const int iincl = wave_incl_scan<false>(ni);
-        const int Q = __builtin_amdgcn_readlane(iincl, 63);
-        const int iexcl = iincl - ni;
-        int icarry = 0;
-        auto item = [&](int Rb, int& pl, int& e) {
-          pl = pair_owner(W->slot, iexcl, ni, Rb, icarry);
-          const int rank = Rb + lane - __builtin_amdgcn_ds_bpermute(pl << 2, iexcl);
-          const unsigned long long ml =
-              ((unsigned long long)(uint32_t)__builtin_amdgcn_ds_bpermute(pl << 2, (int)(uint32_t)(m >> 32)) << 32) |
-              (uint32_t)__builtin_amdgcn_ds_bpermute(pl << 2, (int)(uint32_t)m);
-          const bool v = Rb + lane < Q;
-          e = v ? __builtin_amdgcn_ds_bpermute(pl << 2, c) * 64 + select_bit(ml, rank) : -1;
-          return v;
-        };
-        int ipl = 0, ie = -1;
-        bool iv = Q > 0 && item(0, ipl, ie);
-        float4 tn = iv ? S.cl_tn[ie] : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
-        for (int Rb = 0; Rb < Q; Rb += 64) {
-          const int cpl = ipl, ce = ie;
-          const float4 ct = tn;
-          const bool cv = iv;
-          if (Rb + 64 < Q) {
-            iv = item(Rb + 64, ipl, ie);
-            tn = iv ? S.cl_tn[ie] : make_float4(0.0f, 0.0f, 0.0f, -1.0f);
-          }
-          const f3 rd = mk3(bpermute_f(dd.x, cpl), bpermute_f(dd.y, cpl), bpermute_f(dd.z, cpl));
-          const float rD = bpermute_f(D, cpl);
-          const bool need = cv && danger_needs_test(ct, rd, rD, S.cull_c);
-          if (COUNT) prof_add(WP, PROF_BIG_SWEEPS, 1);
-          if (__any(need)) {
-            if (COUNT) prof_add(WP, PROF_BIG_PASS, 1);
-            const int rl = __builtin_amdgcn_ds_bpermute(cpl << 2, own);  // the pair's ray: lane rl's
-            const f3 ro = mk3(bpermute_f(o.x, rl), bpermute_f(o.y, rl), bpermute_f(o.z, rl));
-            if (need) {
-              const TriData T{S.c_v0[ce], S.c_e1[ce], S.c_e2[ce]};
-              const int orig = fbits(T.e1.w);
-              float bx, by, bzk;
-              const int r = tri_test_v(T, ro, rd, bx, by, bzk);
-              if (r >= 1) atomicMax(&W->lastPass[rl], ((unsigned long long)(unsigned int)(orig + 1) << 32) | f2u(bzk));
-              if (r == 2) {
-                atomicMax(&W->lastHit[rl], orig);
-                atomicAdd(&W->nhit[rl], 1);
-                f3 hp, nn;
-                const float t = tri_hit_t<HYBRID>(S, orig, ro, rd, bx, by, bzk, hp, nn);
-                if (t > 0.0f) atomicMin(&W->best[rl], ((unsigned long long)f2u(t) << 32) | (unsigned int)orig);
+          if (exact) {
+            unsigned long long m = (valid && !hit) ? dm : 0ull;
+            unsigned long long nm = 0ull;  // the danger triangles danger_needs_test keeps
+            if (m) {
+              const float D = box_miss(clo, chi, oo, ii);
+              const int e0 = c * 64;
+              while (m) {  // two normal records per trip: one round trip for both
+                const int k0 = __builtin_ctzll(m);
+                m &= m - 1;
+                const int k1 = m ? __builtin_ctzll(m) : k0;
+                m &= m - 1;
+                const float4 t0 = S.cl_tn[e0 + k0], t1 = S.cl_tn[e0 + k1];
+                if (danger_needs_test(t0, dd, D, S.cull_c)) nm |= 1ull << k0;
+                if (danger_needs_test(t1, dd, D, S.cull_c)) nm |= 1ull << k1;
+              }
+            }
+            if (__any(nm != 0ull)) {  // (rare) glm's u/v tests on the kept ones; a pass sweeps the cluster
+              while (nm && !hit) {
+                const int e = c * 64 + __builtin_ctzll(nm);
+                nm &= nm - 1;
+                float bx, by, bz;
+                hit = tri_test_v(TriData{S.c_v0[e], S.c_e1[e], S.c_e2[e]}, oo, dd, bx, by, bz) >= 1;
               }
             }
           }
         }
         if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
-      }
-      if (COUNT && exact) {
-        wave_lds_sync();
-        if (big) {  // the danger triangles' results folded into the sweeps'
-          const unsigned long long lp = W->lastPass[lane], lb = W->best[lane];
-          k_pass = lp > k_pass ? lp : k_pass;
-          k_lasthit = max(k_lasthit, W->lastHit[lane]);
-          k_nhit += W->nhit[lane];
-          k_best = lb < k_best ? lb : k_best;
-        }
-        wave_lds_sync();  // the LDS slots are rewritten by the small leaves
+        sweep(hit, c, own);
+        if (COUNT) prof_lap(WP, PROF_BIG_CYC);
       }
     }
     if (big) {

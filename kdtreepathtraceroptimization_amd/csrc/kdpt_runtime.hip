@@ -97,7 +97,6 @@ __device__ __attribute__((always_inline)) inline bool gen_rays_body(
       work[k] = 0;
       work[nwork + k] = 0;  // candidate counts (k_geoms), stored after the work counters
       work[2 * nwork + k] = 0;  // k_shade_fused's tile tickets
-      work[3 * nwork + 2 + k] = 0;  // k_trace's cull records (after the two bounce-0 candidate counters)
       trace_t[2 * k] = ~0ull;  // k_trace span of bounce k, then (at 2*nwork) k_geoms' span
       trace_t[2 * k + 1] = 0ull;
       trace_t[2 * nwork + 2 * k] = ~0ull;
@@ -223,8 +222,6 @@ struct TraceArgs {
   Counters* counters;
   unsigned long long* trace_t;  // [4 * cap]: per bounce first block start / last block end (s_memrealtime)
                                 // of k_trace, then of k_geoms (at 2 * cap)
-  unsigned long long* fix_total;  // [2] k_fixup: the exact cull's records and re-traced rays, summed
-  int fix_force;                  // k_fixup re-traces the ray of every record with a danger mask (tests)
 };
 
 struct GenBatch {
@@ -545,7 +542,7 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
   WaveRay R;  // every field defined: idle lanes take part in the wave-level code with a finished ray
   wave_ray_start(S, R, mk3(0.0f, 0.0f, 0.0f), mk3(0.0f, 0.0f, 1.0f), FLT_MAXV, -1, W);
   R.done = true;
-  int pidx = -1;  // the lane's ray: its queue slot in its iteration's candidate list (-1: idle)
+  int pidx = -1;  // the lane's path (-1: idle)
   int pb = 0;     // ... and the batch iteration it belongs to
   // Path slots: each wave first takes a static run of 64 consecutive slots, the runs dealt out wave-major
   // across the workgroups (run r goes to wave r / grid of workgroup r % grid): a bounce with few rays then
@@ -602,11 +599,11 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
           }
         // the slot's path index and its ray (written in queue order with the slot): three independent loads
         // of consecutive slots, not a slot load followed by scattered path loads
+        const int i = cand[local];
         const float4 q0 = cray[2 * local], q1 = cray[2 * local + 1];
-        pidx = local;
+        pidx = i;
         pb = b;
         wave_ray_start(S, R, mk3(q0.x, q0.y, q0.z), mk3(q1.x, q1.y, q1.z), q0.w, fbits(q1.w), W);
-        W->rid[lane] = b << 24 | local;
       }
     }
     if (COUNT) prof_lap(P, PROF_SETUP_CYC);
@@ -658,14 +655,10 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
       const Hit& h = R.h;
       const int code = h.hit_geom_index == -1 ? -1 : (h.obj_intersect ? -(R.objTri + 2) : h.hit_geom_index);
       int2* hits = A.it[0].hits;
-      const int* cand = A.it[0].cand;
 #pragma unroll
       for (int q = 1; q < MAXB; q++)
-        if (pb == q) {
-          hits = A.it[q].hits;
-          cand = A.it[q].cand;
-        }
-      hits[cand[pidx]] = make_int2(code, h.objMaterialIdx);
+        if (pb == q) hits = A.it[q].hits;
+      hits[pidx] = make_int2(code, h.objMaterialIdx);
       pidx = -1;
     }
     if (exhausted && !__any(pidx >= 0)) break;
@@ -696,89 +689,6 @@ __global__ __launch_bounds__(trace_block<MODE>()) KDPT_TRACE_ATTR void k_trace(T
     atomicAdd(&g_tail_prof[1], t1 - (tex < s_t0 ? s_t0 : tex));
     atomicAdd(&g_tail_prof[2], 1ull);
 #endif
-  }
-}
-
-// ---------------------------------------------------------------------------
-// The exact cull's second half.  With direction masks (S.cl_mask) the production k_trace sweeps the clusters
-// whose fast-margin boxes the ray's line meets and records every other (ray, cluster) pair of its big leaves
-// (kdpt_device.h trace_phase).  Each record is decided here: the cluster's danger mask for the ray's direction
-// bucket (kdpt_clusters.h build_dir_masks), then danger_needs_test and glm's u/v tests
-// (gtx/intersect.inl:37-74) on those triangles.  A triangle that passes means the speculative walk may differ
-// from the reference's (a pass moves the hybrid traversal's skip marks and objMaterialIdx even without a
-// hit), so the ray is traced again with traverseKD -- traverseKDbareShortHybrid / traverseKDbare step for
-// step -- and its hit record replaced.  Two records of one ray may both re-trace it: the same deterministic
-// record lands in the same place.  After an overflow of rec_cap every ray of the launch is re-traced.
-// ---------------------------------------------------------------------------
-constexpr int FIXUP_GRID = 2048;
-template <bool HYBRID>
-__global__ __launch_bounds__(256) void k_fixup(TraceArgs A) {
-  const DevScene& S = A.S;
-  const int n = *S.rec_n;
-  const int stride = gridDim.x * blockDim.x;
-  if (blockIdx.x == 0 && threadIdx.x == 0) atomicAdd(&A.fix_total[0], (unsigned long long)n);
-  auto retrace = [&](int b, int local) {
-    atomicAdd(&A.fix_total[1], 1ull);
-    const float4* cray = A.it[0].cray;
-    const int* cand = A.it[0].cand;
-    int2* hits = A.it[0].hits;
-#pragma unroll
-    for (int q = 1; q < MAXB; q++)
-      if (b == q) {
-        cray = A.it[q].cray;
-        cand = A.it[q].cand;
-        hits = A.it[q].hits;
-      }
-    const float4 q0 = cray[2 * local], q1 = cray[2 * local + 1];
-    Ray ray{};
-    ray.origin = mk3(q0.x, q0.y, q0.z);
-    ray.direction = mk3(q1.x, q1.y, q1.z);
-    Hit h{};
-    h.t_min = q0.w;
-    h.hit_geom_index = fbits(q1.w);
-    h.obj_intersect = false;
-    h.objMaterialIdx = -1;
-    h.tri = -1;
-    TraverseCounters cnt{};
-    traverseKD<HYBRID, false>(S, ray, h, S.num_materials, cnt);
-    const int code = h.hit_geom_index == -1 ? -1 : (h.obj_intersect ? -(h.tri + 2) : h.hit_geom_index);
-    hits[cand[local]] = make_int2(code, h.objMaterialIdx);
-  };
-  if (n > S.rec_cap) {  // overflow: the whole launch
-    for (int b = 0; b < A.nb; b++) {
-      const int cnt = A.it[b].ccount[A.depth];
-      for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < cnt; k += stride) retrace(b, k);
-    }
-    return;
-  }
-  const int nbk = 6 * S.mask_n * S.mask_n;
-  for (int r = blockIdx.x * blockDim.x + threadIdx.x; r < n; r += stride) {
-    const int2 e = S.rec[r];
-    const int b = e.x >> 24, local = e.x & 0xffffff, c = e.y;
-    const float4* cray = A.it[0].cray;
-#pragma unroll
-    for (int q = 1; q < MAXB; q++)
-      if (b == q) cray = A.it[q].cray;
-    const float4 q0 = cray[2 * local], q1 = cray[2 * local + 1];
-    const f3 o = mk3(q0.x, q0.y, q0.z), d = mk3(q1.x, q1.y, q1.z);
-    unsigned long long m = S.cl_mask[(size_t)c * nbk + dir_bucket(d, S.mask_n)];
-    if (!m) continue;
-    if (A.fix_force) {
-      retrace(b, local);
-      continue;
-    }
-    const f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
-    const float D = box_miss(S.cl_lo[c], S.cl_hi[c], o, inv);
-    bool redo = false;
-    while (m && !redo) {
-      const int k = __builtin_ctzll(m);
-      m &= m - 1;
-      const int ent = c * 64 + k;
-      if (!danger_needs_test(S.cl_tn[ent], d, D, S.cull_c)) continue;
-      float bx, by, bz;
-      redo = tri_test_v(TriData{S.c_v0[ent], S.c_e1[ent], S.c_e2[ent]}, o, d, bx, by, bz) >= 1;
-    }
-    if (redo) retrace(b, local);
   }
 }
 
@@ -1802,11 +1712,6 @@ struct kdpt_ctx {
   bool shade_batch = true;      // "shade_batch": a batch's fused shading in one launch (k_shade_fused_b)
   bool gen_geoms = true;        // "gen_geoms": camera rays + bounce-0 k_geoms in one launch (k_gen_geoms_b)
   int* ccount0 = nullptr;       // [2] bounce-0 candidate counters of k_gen_geoms_b (alternating uses)
-  int* rec_n = nullptr;         // [cap] k_trace's cull records per bounce (this context leading a launch)
-  int2* rec = nullptr;          // ... the records (k_fixup), allocated when the context first leads one
-  int rec_cap = 0;
-  int rec_cap_knob = 0;         // "rec_cap" tuning knob (> 0: that many records; tests force the overflow)
-  bool fix_force = false;       // "fixup_force" tuning knob: k_fixup re-traces every ray it has a record for
   int gen_parity = 0;           // which of them the next use counts into
   int* cc0_cur = nullptr;       // this use's (bounce 0 reads it instead of ccount[0])
   bool zero_partial = false;    // k_gen_rays zeroes `image` (a pipeline slot's per-iteration partial image)
@@ -1815,8 +1720,7 @@ struct kdpt_ctx {
   Counters last_profile{};
   unsigned long long* total_segments = nullptr;  // device running total (async use)
   unsigned long long* trace_t = nullptr;         // per-bounce intersect launch record (per slot)
-  unsigned long long* trace_total = nullptr;     // [5] device-clock intersect ticks, launches, rays, cull
-                                                 // records, re-traced rays (shared)
+  unsigned long long* trace_total = nullptr;     // [3] device-clock intersect ticks, launches, rays (shared)
   double wall_khz = 100000.0;                    // s_memrealtime frequency
   int* h_counts = nullptr;  // pinned
   hipEvent_t ev0 = nullptr, ev1 = nullptr;
@@ -1931,11 +1835,10 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
     HIP_TRY(hipMemsetAsync(c->buf[b].pm, 0, sizeof(int) * c->npix, c->stream));
   }
   // counts[0..cap+1]: live paths per bounce (rewritten every iteration); counts[cap+2]: fault flag;
-  // counts[cap+3 ..]: work counters of the persistent intersect kernel, candidate counts, tile tickets, the
-  // two bounce-0 candidate counters and the cull record counts
+  // counts[cap+3 ..]: work counters of the persistent intersect kernel
   if ((rc = dalloc(c, &c->trace_t, 4 * (size_t)c->cap))) return rc;
   HIP_TRY(hipMemsetAsync(c->trace_t, 0, sizeof(unsigned long long) * 4 * c->cap, c->stream));
-  if ((rc = dalloc(c, &c->counts, 5 * (size_t)c->cap + 5)) || (rc = dalloc(c, &c->lb, (size_t)c->cap * c->ntiles)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
+  if ((rc = dalloc(c, &c->counts, 4 * (size_t)c->cap + 5)) || (rc = dalloc(c, &c->lb, (size_t)c->cap * c->ntiles)) || (rc = dalloc(c, &c->hits, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->cand, (size_t)c->npix)) || (rc = dalloc(c, &c->prep, (size_t)c->npix)) ||
       (rc = dalloc(c, &c->tile_ccounts, (size_t)c->ntiles)) || (rc = dalloc(c, &c->tile_coff, (size_t)c->ntiles)) ||
       (rc = dalloc(c, &c->cray, 2 * (size_t)c->npix)) ||
@@ -1947,7 +1850,7 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
     return rc;
   if (hipHostMalloc((void**)&c->h_counts, sizeof(int) * (c->cap + 3), hipHostMallocDefault) != hipSuccess)
     return fail(KDPT_ERR_HIP, "hipHostMalloc");
-  HIP_TRY(hipMemsetAsync(c->counts, 0, sizeof(int) * (5 * c->cap + 5), c->stream));
+  HIP_TRY(hipMemsetAsync(c->counts, 0, sizeof(int) * (4 * c->cap + 5), c->stream));
   HIP_TRY(hipMemsetAsync(c->lb, 0, sizeof(unsigned long long) * c->cap * c->ntiles, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->S.fault = c->counts + c->cap + 2;
@@ -1955,7 +1858,6 @@ int alloc_iteration_buffers(kdpt_ctx* c) {
   c->ccount = c->work + c->cap;
   c->tickets = c->ccount + c->cap;
   c->ccount0 = c->tickets + c->cap;  // 2 entries, zero
-  c->rec_n = c->ccount0 + 2;          // cap entries, zeroed by k_gen_rays with the work counters
   c->gen_parity = 0;
   return KDPT_OK;
 }
@@ -2081,8 +1983,13 @@ void apply_cull_route(kdpt_ctx* c) {
 }
 // The direction masks of the scene's clusters at resolution n (cube-map cells per face edge), uploaded.
 int build_masks(kdpt_ctx* c, int n) {
-  std::vector<unsigned long long> m;
-  build_dir_masks(*c->mask_cs, n, c->cull.K, m);
+  std::vector<unsigned long long> cm;
+  build_dir_masks(*c->mask_cs, n, c->cull.K, cm);
+  // bucket-major on the device (DevScene::cl_mask)
+  const size_t ncl = c->mask_cs->info.size(), nb = 6 * (size_t)n * n;
+  std::vector<unsigned long long> m(cm.size());
+  for (size_t k = 0; k < ncl; k++)
+    for (size_t b = 0; b < nb; b++) m[b * ncl + k] = cm[k * nb + b];
   unsigned long long* d = nullptr;
   int rc = dupload(c, &d, m.data(), m.size());
   if (rc) return rc;
@@ -2659,7 +2566,7 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     return bail(rc);
   }
   if ((rc = dalloc(c, &c->counters, 1)) || (rc = dalloc(c, &c->total_segments, 1)) ||
-      (rc = dalloc(c, &c->trace_total, 5)))
+      (rc = dalloc(c, &c->trace_total, 3)))
     return bail(rc);
   {
     int khz = 0;
@@ -2772,7 +2679,8 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     int rc = setup_trace(c);
     if (rc) return rc;
     if (c->grid_env) c->trace_grid = std::max(1, (int)(c->full_trace_grid * frac));
-  } else if (k == "cluster_cull" || k == "cull_margin" || k == "cull_exact" || k == "cull_mask_n") {
+  } else if (k == "cluster_cull" || k == "cull_margin" || k == "cull_exact" || k == "cull_mask_n" ||
+             k == "cull_fast_k") {
     if (k == "cluster_cull") {
       // 0: no cluster / chunk cull at all (every big-leaf cluster swept: exact by construction, whatever the
       // scene's margin); 1: the scene's margins (and masks)
@@ -2788,6 +2696,15 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     } else if (k == "cull_exact") {
       // 0: the fast-margin one-level cull instead of the masked exact one (A/B; not exact for such scenes)
       c->cull_exact = v != 0;
+    } else if (k == "cull_fast_k") {
+      // the masked cull's box coefficient (default CULL_MARGIN_MASKED), its direction masks rebuilt for it: a
+      // wider box sweeps more clusters, a narrower one leaves more danger triangles to decide
+      if (!(value > 0.0 && value < 1.0)) return fail(KDPT_ERR_ARG, "cull_fast_k must be in (0, 1)");
+      if (!c->mask_cs) return fail(KDPT_ERR_ARG, "cull_fast_k: this scene has no direction masks");
+      c->cull.K = c->cull.K_lo = (float)value;
+      if (c->cull_scene) set_cull(c, c->cull);
+      int rc = build_masks(c, c->mask_n);
+      if (rc) return rc;
     } else {
       if (v < 1 || v > 128) return fail(KDPT_ERR_ARG, "cull_mask_n must be in 1 .. 128");
       if (!c->mask_cs) return fail(KDPT_ERR_ARG, "cull_mask_n: this scene has no direction masks");
@@ -2804,15 +2721,7 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     c->profile_steps = v >= 2;
   } else if (k == "sync_debug") {
     c->sync_debug = v != 0;
-  } else if (k == "rec_cap") {
-    // the exact cull's record capacity per intersect launch (0: the default, 4 per ray); a smaller value
-    // forces k_fixup's overflow path (every ray of the launch re-traced) -- tests only
-    if (v < 0) return fail(KDPT_ERR_ARG, "rec_cap must be >= 0");
-    c->rec_cap_knob = v;
-  } else if (k == "fixup_force") {
-    // 1: k_fixup re-traces the ray of every record whose cluster has a danger mask for its direction, pass
-    // or no pass (tests: the re-trace must reproduce the production walk's record)
-    c->fix_force = v != 0;
+
   } else {
     return fail(KDPT_ERR_ARG, "unknown tuning knob " + k);
   }
@@ -2829,7 +2738,7 @@ int kdpt_reset(kdpt_ctx* c) {
   c->intersect_launches_total = 0;
   HIP_TRY(hipMemsetAsync(c->image, 0, sizeof(float) * 3 * (size_t)c->npix, c->stream));
   HIP_TRY(hipMemsetAsync(c->total_segments, 0, sizeof(unsigned long long), c->stream));
-  HIP_TRY(hipMemsetAsync(c->trace_total, 0, 5 * sizeof(unsigned long long), c->stream));
+  HIP_TRY(hipMemsetAsync(c->trace_total, 0, 3 * sizeof(unsigned long long), c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   memset(&c->stats, 0, sizeof c->stats);
   c->stats.intersect_grid_share = 1.0f;
@@ -3105,15 +3014,13 @@ int kdpt_save_hdr(kdpt_ctx* c, const char* path, float samples) {
 int kdpt_get_stats(kdpt_ctx* c, kdpt_stats* st) {
   if (!c || !st) return fail(KDPT_ERR_ARG, "null arg");
   HIP_TRY(hipSetDevice(c->device));
-  unsigned long long tot = 0, tt[5] = {0, 0, 0, 0, 0};
+  unsigned long long tot = 0, tt[3] = {0, 0, 0};
   HIP_TRY(hipMemcpyAsync(&tot, c->total_segments, sizeof tot, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipMemcpyAsync(tt, c->trace_total, sizeof tt, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   c->stats.intersect_device_ms_total = (double)tt[0] / c->wall_khz;
   c->stats.intersect_device_launches_total = (long long)tt[1];
   c->stats.total_trace_rays = (long long)tt[2];
-  c->stats.cull_records_total = (long long)tt[3];
-  c->stats.cull_retraces_total = (long long)tt[4];
   c->stats.total_segments = (long long)tot;
   c->stats.intersect_ms_total = c->intersect_ms_total;
   c->stats.intersect_launches_total = c->intersect_launches_total;
@@ -3462,8 +3369,6 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
     t.depth = depth;
     t.counters = c0->counters;
     t.trace_t = c0->trace_t;
-    t.fix_total = c0->trace_total + 3;
-    t.fix_force = (c0->parent ? c0->parent : c0)->fix_force ? 1 : 0;
     if (c0->viz) {
       for (int b = 0; b < nb; b++) {
         kdpt_ctx* c = cs[b];
@@ -3520,41 +3425,8 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
         hipLaunchKernelGGL(k_geoms_b, dim3((c0->npix + GEN_BLOCK - 1) / GEN_BLOCK, nb), dim3(GEN_BLOCK), 0, st, gb);
         HIP_TRY(hipGetLastError());
       }
-      const bool fixup = t.S.cl_mask && !count;  // the exact cull's records, decided by k_fixup
-      if (fixup) {
-        const kdpt_ctx* root = c0->parent ? c0->parent : c0;
-        const int want = root->rec_cap_knob > 0 ? root->rec_cap_knob
-                                                : (int)std::min<long long>(1ll << 30, 4ll * nb * c0->npix + (1 << 16));
-        if (c0->rec_cap < want) {
-          if (c0->rec) {
-            HIP_TRY(hipStreamSynchronize(st));
-            HIP_TRY(hipFree(c0->rec));
-            c0->allocs.erase(std::find(c0->allocs.begin(), c0->allocs.end(), (void*)c0->rec));
-            c0->rec = nullptr;
-          }
-          int rc = dalloc(c0, &c0->rec, (size_t)want);
-          if (rc) return rc;
-          c0->rec_cap = want;
-        } else if (root->rec_cap_knob > 0) {
-          c0->rec_cap = want;  // (a smaller knob value: the first `want` records of the buffer)
-        }
-        t.S.rec = c0->rec;
-        t.S.rec_n = c0->rec_n + depth;
-        t.S.rec_cap = c0->rec_cap;
-      }
       launch_trace(c0, t, count, st);
       HIP_TRY(hipGetLastError());
-      if (fixup) {
-        if (c0->opt.short_stack) hipLaunchKernelGGL(k_fixup<true>, dim3(FIXUP_GRID), dim3(256), 0, st, t);
-        else hipLaunchKernelGGL(k_fixup<false>, dim3(FIXUP_GRID), dim3(256), 0, st, t);
-        HIP_TRY(hipGetLastError());
-        if (c0->sync_debug) {
-          int nrec = 0;
-          HIP_TRY(hipStreamSynchronize(st));
-          HIP_TRY(hipMemcpy(&nrec, c0->rec_n + depth, sizeof nrec, hipMemcpyDeviceToHost));
-          fprintf(stderr, "[kdpt] depth %d: %d cull records (cap %d)\n", depth, nrec, c0->rec_cap);
-        }
-      }
     }
     if (c0->sync_debug) {
       fprintf(stderr, "[kdpt] trace depth %d launched (grid %d, mode %d, lds %zu, batch %d)\n", depth,

@@ -90,8 +90,7 @@ class Stats(C.Structure):
                 ("total_segments", C.c_longlong), ("intersect_ms_total", C.c_double),
                 ("intersect_launches_total", C.c_longlong), ("intersect_device_ms_total", C.c_double),
                 ("intersect_device_launches_total", C.c_longlong), ("intersect_grid_share", C.c_float),
-                ("total_trace_rays", C.c_longlong), ("cull_records_total", C.c_longlong),
-                ("cull_retraces_total", C.c_longlong)]
+                ("total_trace_rays", C.c_longlong)]
 
 
 class SceneDesc(C.Structure):

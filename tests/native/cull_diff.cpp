@@ -20,6 +20,11 @@
 
 #include "../../kdtreepathtraceroptimization_amd/csrc/kdpt_clusters.h"
 
+// the masked cull's box coefficient and mask resolution: the product's (cluster_margin, dir_mask_resolution)
+// unless MASK_KF / MASK_N say otherwise
+static float mask_kf() { return getenv("MASK_KF") ? (float)atof(getenv("MASK_KF")) : kdpt::CULL_MARGIN_MASKED; }
+static int mask_res(int ncl) { return getenv("MASK_N") ? atoi(getenv("MASK_N")) : kdpt::dir_mask_resolution(ncl); }
+
 using namespace kdpt;
 
 namespace {
@@ -223,10 +228,11 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
             ref_items = 0, ref_back = 0, ref_sw = 0, ref_tris = 0, refq_sw = 0, viol_ref = 0, cmp_rounds = 0,
             cmp_items = 0, viol_cmp = 0, msk_items = 0, msk_pairs = 0, viol_msk = 0, msk_needed = 0, t2_near = 0,
             t2_items = 0, viol_t2 = 0;
-  const int mask_n = getenv("MASK_N") ? atoi(getenv("MASK_N")) : DIR_MASK_N;
+  const int mask_n = mask_res((int)cs.info.size());
+  const float KF = mask_kf();
   const float KD = getenv("MASK_KD") ? (float)atof(getenv("MASK_KD")) : 1e-3f;
   std::vector<unsigned long long> masks, masks2;
-  build_dir_masks(cs, mask_n, CULL_MARGIN_FAST, masks);
+  build_dir_masks(cs, mask_n, KF, masks);
   build_dir_masks(cs, mask_n, KD, masks2);
   std::vector<float4> tn;
   build_entry_normals(cs, tn);
@@ -271,7 +277,7 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
         const bool ok_old = cluster_may_pass(L, H, o, inv, cm.K) &&
                             cluster_may_pass_obb(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ck);
         const float ndv = n.x * d.x + n.y * d.y + n.z * d.z;
-        const float K = cull_k_exact(ndv, cs.kc[c], CULL_MARGIN_FAST);
+        const float K = cull_k_exact(ndv, cs.kc[c], KF);
         if (K < 0) back++;
         else if (-ndv - cs.kc[c].x > 0.0f) front++;
         else graze++;
@@ -281,10 +287,10 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
         // unit normal): back-facing triangles never pass, and a front-facing one needs the margin
         // 17.5 u rho_t / g_t + c (g_t: its determinant bound), or the rigorous one when g_t <= 0
         {
-          const bool fast_ok = cluster_may_pass(L, H, o, inv, CULL_MARGIN_FAST) &&
-                               cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, CULL_MARGIN_FAST);
+          const bool fast_ok = cluster_may_pass(L, H, o, inv, KF) &&
+                               cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, KF);
           bool ok = fast_ok, ok_q = fast_ok;
-          if (!fast_ok && K > CULL_MARGIN_FAST) {
+          if (!fast_ok && K > KF) {
             ref_susp++;
             ref_items += inf.y;
             double Kp = -1, Kq = -1;
@@ -308,7 +314,7 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
                 Kt = g > 0 ? std::min((double)cs.kc[c].z, 17.5 * u * rho / g + cs.kc[c].w) : cs.kc[c].z;
               }
               Kp = std::max(Kp, Kt);
-              const double q = Kt <= CULL_MARGIN_FAST ? CULL_MARGIN_FAST : (Kt <= 1e-3 ? 1e-3 : (Kt <= 1e-2 ? 1e-2 : (double)cs.kc[c].z));
+              const double q = Kt <= KF ? KF : (Kt <= 1e-3 ? 1e-3 : (Kt <= 1e-2 ? 1e-2 : (double)cs.kc[c].z));
               Kq = std::max(Kq, q);
             }
             if (Kp < 0) ref_back++;
@@ -320,7 +326,7 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
           // the compacted design: a pair not culled at the cluster level gets a normal round; every triangle
           // that is front-facing and whose own margin reaches the pair's box is tested in full
           {
-            const bool cheap_cull = K < 0 || (!fast_ok && K <= CULL_MARGIN_FAST) ||
+            const bool cheap_cull = K < 0 || (!fast_ok && K <= KF) ||
                                     !(cluster_may_pass(L, H, o, inv, cs.kc[c].z) &&
                                       cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, cs.kc[c].z));
             if (!cheap_cull) {
@@ -344,7 +350,7 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
                   const double g = -ndt - beta;
                   Kt = g > 0 ? std::min((double)cs.kc[c].z, 17.5 * u * rho / g + cs.kc[c].w) : cs.kc[c].z;
                 }
-                const float Kf = (float)std::max(Kt, (double)CULL_MARGIN_FAST);
+                const float Kf = (float)std::max(Kt, (double)KF);
                 const bool need = cluster_may_pass(L, H, o, inv, Kf) &&
                                   cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, Kf);
                 cmp_items += need;
@@ -483,9 +489,10 @@ int main(int argc, char** argv) {
   const V3 sext = shi - slo;
   const double scale = std::max(sext.x, std::max(sext.y, sext.z));
 
-  const int mask_n = getenv("MASK_N") ? atoi(getenv("MASK_N")) : DIR_MASK_N;
+  const int mask_n = mask_res((int)cs.info.size());
+  const float KF = mask_kf();
   std::vector<unsigned long long> masks;
-  build_dir_masks(cs, mask_n, CULL_MARGIN_FAST, masks);
+  build_dir_masks(cs, mask_n, KF, masks);
   std::vector<float4> tn;
   build_entry_normals(cs, tn);
   Counts tot[NGEN];
@@ -637,9 +644,9 @@ int main(int argc, char** argv) {
         // the triangles of the cluster's danger mask that danger_needs_test keeps; every triangle passing glm's
         // u/v tests must be among them
         const float ndv = cs.nrm[c].x * df.x + cs.nrm[c].y * df.y + cs.nrm[c].z * df.z;
-        const bool hit = cluster_may_pass(L, H, of, inv, CULL_MARGIN_FAST) &&
+        const bool hit = cluster_may_pass(L, H, of, inv, KF) &&
                          cluster_may_pass_obb_k(L, H, cs.nrm[c], cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], of, inv, df, ndv,
-                                                CULL_MARGIN_FAST);
+                                                KF);
         if (!hit) {
           const unsigned long long mk = masks[(size_t)c * 6 * mask_n * mask_n + dir_bucket(df, mask_n)];
           const float Dm = box_miss(L, H, of, inv);
