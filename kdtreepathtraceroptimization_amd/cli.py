@@ -67,7 +67,8 @@ def parse_args(argv=None) -> argparse.Namespace:
     ap.add_argument("--hdr", action="store_true", help="also write BASE.hdr (image::saveHDR)")
     ap.add_argument("--device", type=int, default=0)
     ap.add_argument("--pipeline", type=int, default=8, help="batches in flight (throughput only)")
-    ap.add_argument("--batch", type=int, default=4, help="iterations sharing an intersect launch (<= 8)")
+    ap.add_argument("--batch", type=int, default=16,
+                    help="iterations sharing an intersect launch (<= 16, MAXB); 8 x 16 is bench.py's shape")
     ap.add_argument("--kd-build", choices=["gpu", "host"], default="gpu",
                     help="build the KD tree on the GPU (default; byte-identical) or with the host recursion")
     ap.add_argument("--dry-run", action="store_true", help="load and build the scene, print it, render nothing")
