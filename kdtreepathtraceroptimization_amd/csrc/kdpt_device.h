@@ -1517,10 +1517,11 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       // With direction masks (S.cl_mask: the exact cull, DESIGN.md 4 "Cluster cull") a miss may still hide a
       // u/v pass of a triangle nearly parallel to the line: the cluster's danger mask for the ray's direction
       // bucket (kdpt_clusters.h build_dir_masks) lists every triangle that can need more than cl_margin for
-      // some direction of the bucket.  The missed pair's lane walks those bits itself: each triangle is
-      // decided from its unit normal and the line's box_miss distance (danger_needs_test), and the rare one
-      // that needs it gets glm's u/v tests; a pass turns the miss into a hit, so the whole cluster is swept
-      // like the uncull'd walk would.  (A superset of the clusters with a u/v pass is swept: exact.)
+      // some direction of the bucket.  The mask is requested with the box test and read after the pass's
+      // sweeps (its latency hidden behind them); the missed pair's lane then walks its bits, deciding each
+      // triangle from its unit normal and the line's box_miss distance (danger_needs_test), and the rare one
+      // that needs it gets glm's u/v tests.  A pass sweeps the whole cluster late, as the uncull'd walk would
+      // have: the sweep's results fold by max / min / sum, so a late sweep is the same as an early one.
       const bool exact = S.cl_mask != nullptr;
       const int cfirst = big ? (NodeSrc::kLeafHoldsCluster ? lstart : S.leaf_cl[lnode].x) : 0;
       const int incl = wave_incl_scan<false>(ncl);
@@ -1537,6 +1538,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         const int own = pair_owner(W->slot, excl, ncl, B, carry);
         const int c = W->tbase[own] + B + lane;
         bool hit = B + lane < P;  // (no cull: every pair swept)
+        unsigned long long m = 0ull;  // a missed pair's danger mask (exact cull)
         if (fastAABB) {
           const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
@@ -1558,34 +1560,43 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
                                            cn.x * dd.x + cn.y * dd.y + cn.z * dd.z, S.cl_margin);
             }
           }
-          if (exact) {
-            unsigned long long m = (valid && !hit) ? dm : 0ull;
-            unsigned long long nm = 0ull;  // the danger triangles danger_needs_test keeps
-            if (m) {
-              const float D = box_miss(clo, chi, oo, ii);
-              const int e0 = c * 64;
-              while (m) {  // two normal records per trip: one round trip for both
-                const int k0 = __builtin_ctzll(m);
-                m &= m - 1;
-                const int k1 = m ? __builtin_ctzll(m) : k0;
-                m &= m - 1;
-                const float4 t0 = S.cl_tn[e0 + k0], t1 = S.cl_tn[e0 + k1];
-                if (danger_needs_test(t0, dd, D, S.cull_c)) nm |= 1ull << k0;
-                if (danger_needs_test(t1, dd, D, S.cull_c)) nm |= 1ull << k1;
-              }
+          if (exact && valid && !hit) m = dm;
+        }
+        if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
+        sweep(hit, c, own);
+        if (COUNT) prof_lap(WP, PROF_BIG_CYC);
+        if (!exact || !__any(m != 0ull)) continue;
+        bool late = false;  // a danger triangle passed glm's u/v tests: sweep the cluster now
+        {
+          // (the line, its direction and its box recomputed rather than kept live across the sweep)
+          const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
+          const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
+          const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
+          unsigned long long nm = 0ull;  // the danger triangles danger_needs_test keeps
+          if (m) {
+            const float D = box_miss(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
+            const int e0 = c * 64;
+            while (m) {  // two normal records per trip: one round trip for both
+              const int k0 = __builtin_ctzll(m);
+              m &= m - 1;
+              const int k1 = m ? __builtin_ctzll(m) : k0;
+              m &= m - 1;
+              const float4 t0 = S.cl_tn[e0 + k0], t1 = S.cl_tn[e0 + k1];
+              if (danger_needs_test(t0, dd, D, S.cull_c)) nm |= 1ull << k0;
+              if (danger_needs_test(t1, dd, D, S.cull_c)) nm |= 1ull << k1;
             }
-            if (__any(nm != 0ull)) {  // (rare) glm's u/v tests on the kept ones; a pass sweeps the cluster
-              while (nm && !hit) {
-                const int e = c * 64 + __builtin_ctzll(nm);
-                nm &= nm - 1;
-                float bx, by, bz;
-                hit = tri_test_v(TriData{S.c_v0[e], S.c_e1[e], S.c_e2[e]}, oo, dd, bx, by, bz) >= 1;
-              }
+          }
+          if (__any(nm != 0ull)) {  // (rare) glm's u/v tests on the kept ones
+            while (nm && !late) {
+              const int e = c * 64 + __builtin_ctzll(nm);
+              nm &= nm - 1;
+              float bx, by, bz;
+              late = tri_test_v(TriData{S.c_v0[e], S.c_e1[e], S.c_e2[e]}, oo, dd, bx, by, bz) >= 1;
             }
           }
         }
         if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
-        sweep(hit, c, own);
+        if (__any(late)) sweep(late, c, own);
         if (COUNT) prof_lap(WP, PROF_BIG_CYC);
       }
     }

@@ -19,6 +19,8 @@ for res in RES:
     p = pt.wave_profile()
     w = max(1, p["chunks"])
     life = p.pop("wave_life_10us", [])
+    for k in ("ray_steps_hist4", "chord_steps", "chord_rays"):
+        p.pop(k, None)
     per_chunk = {k: round(v / w, 1) for k, v in p.items() if k != "chunks"}
     kc = max(1, p["chunk_cycles"])
     frac = {k: round(p[k] / kc, 3) for k in p if k.endswith("_cycles") and k != "chunk_cycles"}
