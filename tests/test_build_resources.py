@@ -47,13 +47,13 @@ HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_traceILb1ELb0ELi
 # Batches of up to 16 iterations per intersect launch (MAXB) cost the derived-box routes a few more bytes.
 # TREE_LDS16 (mode 3: derived records with the cluster boxes in LDS, e.g. the level-6 icosphere) measured
 # 60 / 44 B with MAXB 16.
-# The masked exact cull (round 5: a missed pair's lane walks its danger mask, two normal records per trip) keeps
-# the pair's line, box and mask live across the oriented-box test: +12 B on the LDS-tree route C3 runs (mode 2),
-# +40-50 B on the derived-record routes (modes 3 / 4) that carry the masked cull for larger trees; the C5 route
-# (mode 5, no masks) is unchanged.  Measured with the spills: profiles/r05_ab_log.md.
-SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 48, "k_traceILb0ELb0ELi2E": 48, "k_traceILb1ELb0ELi3E": 120,
-              "k_traceILb0ELb0ELi3E": 120, "k_traceILb1ELb0ELi4E": 104,
-              "k_traceILb0ELb0ELi4E": 104, "k_traceILb1ELb0ELi5E": 116, "k_traceILb0ELb0ELi5E": 116,
+# The masked exact cull (round 5: a missed pair's danger mask is requested with the box test and walked after the
+# pass's sweeps, two normal records per trip) keeps the mask live across the sweep: +4 B on the LDS-tree route C3
+# runs (mode 2), +30-40 B on the derived-record routes (modes 3 / 4) that carry the masked cull for larger trees;
+# the C5 route (mode 5, no masks) is unchanged.  Measured with the spills: profiles/r05_ab_log.md.
+SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 40, "k_traceILb0ELb0ELi2E": 40, "k_traceILb1ELb0ELi3E": 104,
+              "k_traceILb0ELb0ELi3E": 104, "k_traceILb1ELb0ELi4E": 92,
+              "k_traceILb0ELb0ELi4E": 92, "k_traceILb1ELb0ELi5E": 116, "k_traceILb0ELb0ELi5E": 116,
               "k_shade_fused": 28}
 
 
