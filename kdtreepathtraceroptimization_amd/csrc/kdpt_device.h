@@ -581,6 +581,15 @@ KDPT_HD bool cluster_may_pass_obb(float4 lo, float4 hi, float4 n, float4 u, floa
 // directions (grown by 1e-5 in u and v, far above this function's rounding), so any float d maps to a cell
 // whose bound holds it.  Any finite nonzero d works (the cull only runs for lanes whose 1 / d components are
 // all finite).
+// 1 / x for box_miss and dir_bucket: the hardware reciprocal (1 ulp) on the device, the division on the host;
+// box_miss's 1e-5 slack and the masks' 1e-5 cell growth cover either
+KDPT_HD inline float kd_rcp(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+  return __builtin_amdgcn_rcpf(x);
+#else
+  return 1.0f / x;
+#endif
+}
 KDPT_HD int dir_bucket(f3 d, int n) {
   const float ax = fabsf(d.x), ay = fabsf(d.y), az = fabsf(d.z);
   int face;
@@ -601,7 +610,7 @@ KDPT_HD int dir_bucket(f3 d, int n) {
     b = d.y;
     m = az;
   }
-  const float h = 0.5f * (float)n / m;
+  const float h = 0.5f * (float)n * kd_rcp(m);
   int i = (int)((a + m) * h), j = (int)((b + m) * h);
   i = i < 0 ? 0 : (i > n - 1 ? n - 1 : i);
   j = j < 0 ? 0 : (j > n - 1 ? n - 1 : j);
@@ -625,11 +634,11 @@ KDPT_HD float box_miss(float4 lo, float4 hi, f3 o, f3 inv) {
   const float ax = fminf(tlx, thx), bx = fmaxf(tlx, thx), ay = fminf(tly, thy), by = fmaxf(tly, thy);
   const float az = fminf(tlz, thz), bz = fmaxf(tlz, thz);
   const float wx = fabsf(inv.x), wy = fabsf(inv.y), wz = fabsf(inv.z);
-  const float mxy = fmaxf(ax - by, ay - bx) / (wx + wy);
-  const float mxz = fmaxf(ax - bz, az - bx) / (wx + wz);
-  const float myz = fmaxf(ay - bz, az - by) / (wy + wz);
+  const float mxy = fmaxf(ax - by, ay - bx) * kd_rcp(wx + wy);
+  const float mxz = fmaxf(ax - bz, az - bx) * kd_rcp(wx + wz);
+  const float myz = fmaxf(ay - bz, az - by) * kd_rcp(wy + wz);
   const float m = fmaxf(0.0f, fmaxf(mxy, fmaxf(mxz, myz)));
-  return m / W * 0.99999f;
+  return m * kd_rcp(W) * 0.99999f;
 }
 
 // The exact cull's per-triangle decision for a (line, cluster) pair whose line misses the cluster's box by D
@@ -1540,9 +1549,10 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         bool hit = B + lane < P;  // (no cull: every pair swept)
         unsigned long long m = 0ull;  // a missed pair's danger mask (exact cull)
         if (fastAABB) {
-          const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
+          const float4 od = W->od[own];  // the pair's ray from the wave's LDS copy (wave_ray_start)
+          const float2 d2 = W->dd[own];
+          const f3 oo = mk3(od.x, od.y, od.z), dd = mk3(od.w, d2.x, d2.y);
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
-          const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
           float4 clo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), chi = clo;
           unsigned long long dm = 0ull;
           const bool valid = hit;
@@ -1569,9 +1579,10 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         bool late = false;  // a danger triangle passed glm's u/v tests: sweep the cluster now
         {
           // (the line, its direction and its box recomputed rather than kept live across the sweep)
-          const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
+          const float4 od = W->od[own];  // the pair's ray from the wave's LDS copy (wave_ray_start)
+          const float2 d2 = W->dd[own];
+          const f3 oo = mk3(od.x, od.y, od.z), dd = mk3(od.w, d2.x, d2.y);
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
-          const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
           unsigned long long nm = 0ull;  // the danger triangles danger_needs_test keeps
           if (m) {
             const float D = box_miss(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
