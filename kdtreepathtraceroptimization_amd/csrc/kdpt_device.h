@@ -1455,13 +1455,15 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         }
         if (pass) sinfo = clusters.sup(sp, slo, shi);
         if (fastAABB) {
-          const f3 oo = mk3(bpermute_f(o.x, own), bpermute_f(o.y, own), bpermute_f(o.z, own));
+          const float4 od = W->od[own];  // the pair's ray from the wave's LDS copy (wave_ray_start)
+          const f3 oo = mk3(od.x, od.y, od.z);
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
           if (pass) pass = cluster_may_pass(slo, shi, oo, ii, S.cl_margin);
           // the boxes' survivors against the super's slab (its record from L2), with the margin its normal
           // spread allows for this direction
           if (S.sup_slab && __any(pass)) {
-            const f3 dd = mk3(bpermute_f(d.x, own), bpermute_f(d.y, own), bpermute_f(d.z, own));
+            const float2 d2 = W->dd[own];
+            const f3 dd = mk3(od.w, d2.x, d2.y);
             const CullK ck{S.cl_margin, S.cl_margin_lo, S.cull_a, S.cull_b, S.cull_c};
             if (pass) {
               pass = cluster_may_pass_slab(make_float4(slo.x, slo.y, slo.z, sb.x), make_float4(shi.x, shi.y, shi.z, sb.y),
@@ -1497,12 +1499,14 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
               rv = clusters.v[c];
               rw = clusters.w[c];
             }
-            const f3 oo = mk3(bpermute_f(o.x, cown), bpermute_f(o.y, cown), bpermute_f(o.z, cown));
+            const float4 od = W->od[cown];
+            const f3 oo = mk3(od.x, od.y, od.z);
             const f3 ii =
                 mk3(bpermute_f(invdir.x, cown), bpermute_f(invdir.y, cown), bpermute_f(invdir.z, cown));
             if (S.cl_slab) {
               const CullK ck{S.cl_margin, S.cl_margin_lo, S.cull_a, S.cull_b, S.cull_c};
-              const f3 dd = mk3(bpermute_f(d.x, cown), bpermute_f(d.y, cown), bpermute_f(d.z, cown));
+              const float2 d2 = W->dd[cown];
+              const f3 dd = mk3(od.w, d2.x, d2.y);
               if (cp) {
                 if (S.cl_obb)
                   cp = cluster_may_pass_obb(rlo, rhi, rn, ru, rv, rw, oo, ii, dd, ck);
