@@ -583,7 +583,7 @@ KDPT_HD bool cluster_may_pass_obb(float4 lo, float4 hi, float4 n, float4 u, floa
 // all finite).
 // 1 / x for box_miss and dir_bucket: the hardware reciprocal (1 ulp) on the device, the division on the host;
 // box_miss's 1e-5 slack and the masks' 1e-5 cell growth cover either
-KDPT_HD inline float kd_rcp(float x) {
+KDPT_HD float kd_rcp(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_rcpf(x);
 #else
