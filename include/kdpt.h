@@ -241,8 +241,11 @@ int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
  * "flat_obb" (1; 0 = the one-level cluster cull tests the clusters' axis-aligned boxes only, not also
  * their oriented boxes),
  * "cluster_cull" (1; 0 = no cluster / chunk cull at all: every big-leaf cluster is swept, exact by
- * construction), "cull_margin" (0 = the scene's; > 0 overrides the cull's margin coefficient),
- * "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots (they are remade). */
+ * construction), "cull_margin" (0 = the scene's; > 0 overrides the cull's margin coefficient, no masks),
+ * "cull_exact" (1; 0 = for meshes of large triangles the margin-only cull instead of the masked exact one, not
+ * exact), "cull_mask_n" (the direction masks' cube-map cells per face edge, 1 .. 128; default: the finest of
+ * 128 / 64 / 32 ... within 160 MB), "cull_fast_k" (the masked cull's box coefficient, default 1e-3; the masks
+ * are rebuilt for it), "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots (they are remade). */
 int kdpt_set_tuning(kdpt_ctx *ctx, const char *name, double value);
 /* The intersect kernel's configuration: tree source (0 HBM 64-byte records, 1 HBM 32-byte, 2 LDS 32-byte,
  * 3 LDS 16-byte derived-box records + cluster boxes, 4 LDS 16-byte records with cluster boxes in HBM,
@@ -253,8 +256,10 @@ int kdpt_trace_config(kdpt_ctx *ctx, int *tree_mode, int *block, int *grid, long
 /* The big-leaf cluster cull (and the brute-force chunk cull): the margin coefficient in use, the scene's
  * rigorous coefficient, and exact = 1 when the one in use is >= the rigorous one -- the cull then never
  * drops a cluster holding a triangle that passes glm's u/v tests, for any ray ("Cluster cull").
- * exact = 0: the scene's triangles are too large for a rigorous margin that still culls; the cull is then
- * conservative except for rays nearly coplanar with a triangle (tuning "cluster_cull" = 0 removes it). */
+ * For meshes whose triangles are too large for a rigorous margin that still culls (dragon_5), the box levels
+ * use a fast coefficient and per-cluster direction masks decide the missed pairs' near-parallel triangles
+ * one by one (the masked cull): exact = 1 as well.  exact = 0 only after tuning "cull_exact" = 0 or a fixed
+ * "cull_margin": the cull is then conservative except for rays nearly coplanar with a triangle. */
 int kdpt_cull_margin(kdpt_ctx *ctx, float *margin, double *rigorous, int *exact);
 
 /* ---- Multi-GPU: samples per pixel sharded across GPUs ----
