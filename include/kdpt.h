@@ -228,7 +228,7 @@ int kdpt_get_stats(kdpt_ctx *ctx, kdpt_stats *st);
 int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
 /* Explicit A/B and diagnostic knobs (the library reads no environment variables; a context created
  * without this call always runs the tested default route).  Names: "shade_fused" (1; 0 = k_shade +
- * k_scan + k_scatter), "early_walk" (24) / "early_leaf" (1) (node-phase hand-over thresholds),
+ * k_scan + k_scatter), "early_walk" (16) / "early_leaf" (1) (node-phase hand-over thresholds),
  * "chunk_width0..2" (16, 64, 64), "trace_grid_frac" (grid share of every intersect launch, (0, 1]),
  * "tree_global" (0; 1 = KD tree read from HBM/L2 instead of LDS), "profile_batches" (0; 1 = counting intersect kernel for kdpt_wave_profile, 2 = also its
  * per-ray node-step histogram),

@@ -2579,8 +2579,11 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   // leave the node phase early once at most early_walk lanes still walk and at least early_leaf wait on a
   // leaf (the walkers resume after the leaf phase; first A/B at 32 / 24: 3 390 -> 3 540 Mrays/s; 0 / 65 =
   // never)
-  c->S.early_walk = 24;  // re-swept after the flattened leaf phase made leaf phases cheaper (32 / 24 before):
-  c->S.early_leaf = 1;   // 4 505-4 530 -> 4 659-4 704 Mrays/s, k_trace launch 0.85 -> 0.80 ms
+  // re-swept after the flattened leaf phase made leaf phases cheaper (32 / 24 before: 4 505-4 530 -> 4 659-4 704
+  // Mrays/s, k_trace launch 0.85 -> 0.80 ms), and again with round 5's exact cull (24 -> 16: C3 5 747-5 756 ->
+  // 5 798-5 802, C5 4 487 -> 4 544; 8 / 12 / 20 / 32 below 16, early_leaf 8 / 24 neutral; profiles/r05_ab_log.md)
+  c->S.early_walk = 16;
+  c->S.early_leaf = 1;
   c->trace_order = false;  // superseded by k_geoms' candidate lists
   if ((rc = setup_trace(c))) return bail(rc);
   c->S.trip_limit = 8 * std::max(c->S.num_nodes, 1) + 64;
