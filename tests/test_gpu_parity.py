@@ -329,9 +329,12 @@ def test_tuning_knobs_keep_parity(kdpt):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("mesh,res,depth,cap,iters", [("dragon_5", (800, 800), 8, 8, 16),
-                                                      ("icosphere_8", (1600, 1600), 16, 16, 2)])
-def test_cluster_cull_equals_no_cull_at_scale(kdpt, mesh, res, depth, cap, iters):
+@pytest.mark.parametrize("mesh,res,depth,cap,iters,knobs", [("dragon_5", (800, 800), 8, 8, 16, {}),
+                                                            ("dragon_5", (800, 800), 8, 8, 8,
+                                                             {"cull_mask_n": 32, "cull_fast_k": 1e-4}),
+                                                            ("icosphere_8", (1600, 1600), 16, 16, 2, {})],
+                         ids=["c3", "c3-masks32-k1e-4", "c5"])
+def test_cluster_cull_equals_no_cull_at_scale(kdpt, mesh, res, depth, cap, iters, knobs):
     """The cluster cull (default margin) against no cull at all (tuning cluster_cull = 0: every cluster of
     every visited big leaf swept, the reference's semantics by construction) on the headline workloads at
     full size: C3 (dragon_5, 800^2, 16 iterations, ~40 M segments) and C5 (the 1.31 M-triangle icosphere,
@@ -344,6 +347,8 @@ def test_cluster_cull_equals_no_cull_at_scale(kdpt, mesh, res, depth, cap, iters
     imgs, segs, info = [], [], None
     for cull in (1, 0):
         with kdpt.PathTracer(sd, kdpt.default_options(bounce_cap=cap)) as pt:
+            for k, v in knobs.items():  # (the masked cull at round 5's first resolution and box coefficient)
+                pt.set_tuning(k, v)
             if info is None:
                 info = pt.cull_margin()
             pt.set_tuning("cluster_cull", cull)
