@@ -178,6 +178,8 @@ typedef struct kdpt_stats {
                                     kdpt_trace_iterations (1 for one-at-a-time tracing) */
     long long total_trace_rays;  /* since create/reset: rays handed to the KD traversal kernel (k_trace), i.e.
                                     the segments whose ray meets the KD root box */
+    double create_ms;            /* host wall time of kdpt_create (uploads, cluster build, masks, kernel setup) */
+    double mask_build_ms;        /* ... of which the masked cull's direction masks (built on the device; 0: none) */
 } kdpt_stats;
 
 typedef struct kdpt_ctx kdpt_ctx;
@@ -245,7 +247,12 @@ int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
  * "cull_exact" (1; 0 = for meshes of large triangles the margin-only cull instead of the masked exact one, not
  * exact), "cull_mask_n" (the direction masks' cube-map cells per face edge, 1 .. 128; default: the finest of
  * 128 / 64 / 32 ... within 160 MB), "cull_fast_k" (the masked cull's box coefficient, default 1e-3; the masks
- * are rebuilt for it), "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots (they are remade). */
+ * are rebuilt for it), "cull_bound" (1; 0 = the masked cull reads every missed pair's danger mask instead of first
+ * testing the line against its cell's bound, exact either way), "reduce_spin_us" (0; > 0: a device spin of that many
+ * microseconds on the reduce stream before every frame's reduce, emulating an ncclReduce that waits for a slower
+ * peer -- a diagnostic of the frame pipeline; ctx = NULL sets it for contexts created later, e.g. the ones
+ * kdpt_render_sharded creates), "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots
+ * (they are remade). */
 int kdpt_set_tuning(kdpt_ctx *ctx, const char *name, double value);
 /* The intersect kernel's configuration: tree source (0 HBM 64-byte records, 1 HBM 32-byte, 2 LDS 32-byte,
  * 3 LDS 16-byte derived-box records + cluster boxes, 4 LDS 16-byte records with cluster boxes in HBM,
@@ -258,9 +265,16 @@ int kdpt_trace_config(kdpt_ctx *ctx, int *tree_mode, int *block, int *grid, long
  * drops a cluster holding a triangle that passes glm's u/v tests, for any ray ("Cluster cull").
  * For meshes whose triangles are too large for a rigorous margin that still culls (dragon_5), the box levels
  * use a fast coefficient and per-cluster direction masks decide the missed pairs' near-parallel triangles
- * one by one (the masked cull): exact = 1 as well.  exact = 0 only after tuning "cull_exact" = 0 or a fixed
- * "cull_margin": the cull is then conservative except for rays nearly coplanar with a triangle. */
+ * one by one (the masked cull): exact = 1 as well.  exact = 0 after tuning "cull_exact" = 0 or a fixed
+ * "cull_margin", and for the brute-force route (enable_kd = 0) of such meshes, whose 64-triangle chunk boxes are
+ * culled at the box coefficient (1e-3) without masks: the cull is then conservative except for rays nearly
+ * coplanar with a triangle. */
 int kdpt_cull_margin(kdpt_ctx *ctx, float *margin, double *rigorous, int *exact);
+/* The masked cull's tables as the device built them (bucket-major: cell b * num_clusters + c, 6 mask_n^2 buckets):
+ * danger masks and bound codes.  *mask_n = 0 when the scene has none (its cull is exact without them).  masks /
+ * codes may be NULL (sizes only); otherwise 6 mask_n^2 num_clusters entries each.  For parity tests against the
+ * host builder (kdpt_clusters.h build_dir_masks). */
+int kdpt_cull_masks(kdpt_ctx *ctx, int *mask_n, int *num_clusters, unsigned long long *masks, uint8_t *codes);
 
 /* ---- Multi-GPU: samples per pixel sharded across GPUs ----
  * Frame f covers global iterations f*spp + 1 .. (f+1)*spp (the RNG seeds, iteration 2's sort and cacherays
@@ -276,7 +290,9 @@ int kdpt_cull_margin(kdpt_ctx *ctx, float *margin, double *rigorous, int *exact)
 #define KDPT_REDUCE_RCCL 0  /* ncclReduce (one communicator rank per context) */
 #define KDPT_REDUCE_COPY 1  /* in-process: peer copies to the first device, added in rank order */
 /* One process per GPU: rank 0 makes the id, the caller hands it to every rank (any channel), and each rank
- * joins with its context (collective: every rank must call it).  id = NULL with nranks > 1: no
+ * joins with its context (collective: every rank must call it).  An id is single-use: every communicator (every
+ * kdpt_comm_init round over the ranks) needs a fresh kdpt_comm_unique_id -- reusing one makes RCCL fail
+ * ("remote process exited or there was a network error").  id = NULL with nranks > 1: no
  * communicator; kdpt_render_frames then copies every rank's frame shares to its `out` and the caller reduces
  * them (e.g. over gloo when ranks share a GPU, which RCCL refuses); the image is left alone. */
 int kdpt_comm_unique_id(unsigned char *id);
@@ -288,7 +304,8 @@ int kdpt_comm_library(char *path, int len);
 /* This rank's share of frames first_frame .. first_frame + frames - 1 (every rank calls it with the same
  * arguments); out: rank 0, frames * 3*W*H floats, device or host memory, or NULL. */
 int kdpt_render_frames(kdpt_ctx *ctx, int first_frame, int frames, int spp, int pipeline, int batch, float *out);
-/* (a pageable host `out` is pinned for the copies -- hipHostRegister -- until kdpt_synchronize) */
+/* (a pageable host `out` is pinned for the copies -- hipHostRegister -- until kdpt_synchronize; it must stay
+ * allocated until kdpt_synchronize returns, and two contexts must not render into one `out` range at once) */
 /* One process, one context per device (devices[0..ndev), <= 8; a device may repeat with KDPT_REDUCE_COPY):
  * renders the frames, waits, and frees everything.  out (host or device 0 memory, frames * 3*W*H floats, or
  * NULL) receives each frame's reduced image. */

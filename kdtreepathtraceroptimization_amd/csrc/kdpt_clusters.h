@@ -442,9 +442,10 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
 }
 
 // Direction masks of the exact one-level cull (DevScene::cl_mask).  For every cluster c and direction bucket b
-// (dir_bucket: a cube map of n x n cells per face, nb = 6 n^2 buckets), out[c nb + b] = the danger mask over the
-// cluster's 64 entries: the triangles that, for SOME direction of the bucket, are front-facing and need a margin
-// above Kf -- the coefficient of the fast box test a pair's line missed.  A triangle t needs the margin
+// (dir_bucket: a cube map of n x n cells per face, nb = 6 n^2 buckets), masks[b ncl + c] = the danger mask over
+// the cluster's 64 entries: the triangles that, for SOME direction of the bucket, are front-facing and need a
+// margin above Kf -- the coefficient of the fast box test a pair's line missed (and whose rigorous coefficient
+// exceeds Kf; codes[b ncl + c] bounds those coefficients, mask_bound_code).  A triangle t needs the margin
 // K_t(d) = 17.5 u rho_t / g_t + c (g_t = -N_t/|N_t| . d - beta_t; danger_needs_test), above Kf only when
 // g_t < 17.5 u rho_t / (Kf - c).  Every other triangle of such a cluster is back-facing for the whole bucket
 // (its float determinant negative) or lies farther from the line than its own error bound: it cannot pass glm's
@@ -454,15 +455,26 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
 // So |N . d - N . d_b| <= r_b (+ 1e-6 for the float d's length).  Exactly degenerate triangles are in every mask
 // when |e1||e2| > 0.3 and in none otherwise (their float determinant stays below FLT_EPSILON).
 constexpr int DIR_MASK_N = 128;  // finest cube-map cells per face edge (6 n^2 buckets; dir_mask_resolution)
-inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<unsigned long long>& out) {
-  const int ncl = (int)cs.info.size(), nb = 6 * n * n;
-  out.assign((size_t)nb * ncl, 0ull);
-  const double u = ULP_HALF, grow = 1e-5;
-  // per entry (structure of arrays): the unit normal and the two thresholds on x = N . d_b -- front when
-  // x - r <= beta, danger when also x + r >= dthr.  Entries in every mask get (0, inf, -inf), entries in none
-  // (padding, exactly degenerate with |e1||e2| <= 0.3) (0, -inf, -)
+
+// Per cluster entry of the masked cull (structure of arrays, 64 entries per cluster; dir_mask_cell): the unit
+// normal and the two thresholds on x = N . d_b -- front when x - r <= beta, danger when also x + r >= dthr --
+// and the rigorous coefficient krig = 8.75 |e1||e2| + c (c: the cluster's, ClusterSet::kc.w), rounded up.
+// Entries in every mask get (0, inf, -inf), entries in none (padding, exactly degenerate with |e1||e2| <= 0.3)
+// (0, -inf, -).
+struct MaskEntries {
+  std::vector<double> nx, ny, nz, beta, dthr;
+  std::vector<float> krig;
+};
+inline void mask_entries(const ClusterSet& cs, float Kf, MaskEntries& me) {
+  const int ncl = (int)cs.info.size();
   const size_t ne = 64 * (size_t)ncl;
-  std::vector<double> nx(ne, 0.0), ny(ne, 0.0), nz(ne, 0.0), beta(ne, -HUGE_VAL), dthr(ne, HUGE_VAL);
+  const double u = ULP_HALF;
+  me.nx.assign(ne, 0.0);
+  me.ny.assign(ne, 0.0);
+  me.nz.assign(ne, 0.0);
+  me.beta.assign(ne, -HUGE_VAL);
+  me.dthr.assign(ne, HUGE_VAL);
+  me.krig.assign(ne, 0.0f);
   for (int c = 0; c < ncl; c++) {
     const int2 inf = cs.info[c];
     const double gden = (double)Kf - cs.kc[c].w;
@@ -474,24 +486,30 @@ inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<u
       const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
       const double la = std::sqrt((double)e1.x * e1.x + (double)e1.y * e1.y + (double)e1.z * e1.z);
       const double lb = std::sqrt((double)e2.x * e2.x + (double)e2.y * e2.y + (double)e2.z * e2.z);
+      me.krig[q] = std::nextafter((float)(8.75 * la * lb + (double)cs.kc[c].w), HUGE_VALF);
       if (Nl == 0.0) {
         if (la * lb > 0.3) {
-          beta[q] = HUGE_VAL;
-          dthr[q] = -HUGE_VAL;
+          me.beta[q] = HUGE_VAL;
+          me.dthr[q] = -HUGE_VAL;
         }
         continue;
       }
       const double rho = std::max(1.0, la * lb / Nl);
-      nx[q] = Nx / Nl;
-      ny[q] = Ny / Nl;
-      nz[q] = Nz / Nl;
-      beta[q] = 5.8 * u * rho * (1.0 + 1e-3) + 40.0 * u;
+      me.nx[q] = Nx / Nl;
+      me.ny[q] = Ny / Nl;
+      me.nz[q] = Nz / Nl;
+      me.beta[q] = 5.8 * u * rho * (1.0 + 1e-3) + 40.0 * u;
       const double gamma = gden > 0 ? 17.5 * u * rho * (1.0 + 1e-5) / gden : HUGE_VAL;
-      dthr[q] = -beta[q] - gamma;
+      me.dthr[q] = -me.beta[q] - gamma;
     }
   }
-  // the buckets' centre directions and radii
-  std::vector<double> bd(4 * (size_t)nb);
+}
+
+// The buckets' centre directions and radii (4 doubles per bucket, dir_mask_cell's D).
+inline void mask_buckets(int n, std::vector<double>& bd) {
+  const int nb = 6 * n * n;
+  const double grow = 1e-5;
+  bd.assign(4 * (size_t)nb, 0.0);
   for (int b = 0; b < nb; b++) {
     const int face = b / (n * n), j = (b / n) % n, i = b % n;
     const double a0 = -1.0 + 2.0 * i / n - grow, a1 = -1.0 + 2.0 * (i + 1) / n + grow;
@@ -509,27 +527,43 @@ inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<u
     const double dl = std::sqrt(D[0] * D[0] + D[1] * D[1] + D[2] * D[2]);
     for (int a = 0; a < 3; a++) D[a] /= dl;
   }
-  // cluster-major: a cluster's 64 entries stay in cache over its buckets
-  auto work = [&](int c) {
+}
+
+// The masks and their bound codes on the host, bucket-major (masks[b ncl + c], codes likewise: DevScene::cl_mask,
+// cl_mq).  Test infrastructure: the product builds the same cells on the device (kdpt_runtime.hip k_build_masks,
+// the same dir_mask_cell over the same entries and buckets; tests/test_gpu_parity.py compares the two).
+inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<unsigned long long>& masks,
+                            std::vector<unsigned char>& codes) {
+  const int ncl = (int)cs.info.size(), nb = 6 * n * n;
+  MaskEntries me;
+  mask_entries(cs, Kf, me);
+  std::vector<double> bd;
+  mask_buckets(n, bd);
+  masks.assign((size_t)nb * ncl, 0ull);
+  codes.assign((size_t)nb * ncl, 0);
+  auto work = [&](int c) {  // cluster by cluster: its 64 entries stay in cache over the buckets
     const size_t q0 = 64 * (size_t)c;
     for (int b = 0; b < nb; b++) {
-      const double* D = &bd[4 * (size_t)b];
-      unsigned long long md = 0;
-      for (int k = 0; k < 64; k++) {
-        const size_t q = q0 + k;
-        const double x = nx[q] * D[0] + ny[q] * D[1] + nz[q] * D[2];
-        // front-facing for some direction of the bucket, and needing more than Kf for some direction of it
-        md |= (unsigned long long)(x - D[3] <= beta[q] && x + D[3] >= dthr[q]) << k;
-      }
-      out[(size_t)c * nb + b] = md;
+      unsigned long long md;
+      uint32_t code;
+      dir_mask_cell(&me.nx[q0], &me.ny[q0], &me.nz[q0], &me.beta[q0], &me.dthr[q0], &me.krig[q0], &bd[4 * (size_t)b],
+                    Kf, md, code);
+      masks[(size_t)b * ncl + c] = md;
+      codes[(size_t)b * ncl + c] = (unsigned char)code;
     }
   };
   const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   std::vector<std::thread> th;
-  for (int t = 0; t < nth; t++)
-    th.emplace_back([&, t]() {
-      for (int c = t; c < ncl; c += nth) work(c);
-    });
+  int started = 0;
+  try {
+    for (; started < nth; started++)
+      th.emplace_back([&, started]() {
+        for (int c = started; c < ncl; c += nth) work(c);
+      });
+  } catch (...) {  // no thread could be started: the remaining residues run here
+  }
+  for (int t = started; t < nth; t++)
+    for (int c = t; c < ncl; c += nth) work(c);
   for (auto& x : th) x.join();
 }
 
@@ -611,9 +645,11 @@ inline void build_chunk_boxes(const std::vector<float4>& tv, const std::vector<f
 // = 2u that is 8.67 |o - v0| E + ..., E = |e1| |e2|.  So K_rigorous = 8.75 E_max + 64 u (1 + max|coord| +
 // max|e|) makes the cull conservative for EVERY line (the constant term covers the box and slab tests' own
 // rounding).  Meshes of small triangles (the C5 icosphere: E_max = 1.07e-4, K = 9.4e-4) get it; for meshes of
-// large triangles it would cull nothing (dragon_5: E_max = 0.2), so they keep K = 1e-4, conservative except
-// for lines lying within ~17 u |o - v0| of a triangle's plane and within ~17 u rho / K of parallel to it
-// (tests/native/cull_diff.cpp constructs such lines); the "cluster_cull" knob = 0 removes the cull.
+// large triangles it would cull nothing (dragon_5: E_max = 0.2), so their box levels use K = CULL_MARGIN_MASKED
+// (1e-3) and the masked cull (build_dir_masks, mask_bound_code) decides a missed pair's near-parallel triangles:
+// exact as well.  The box coefficient alone (knob "cull_exact" = 0, and the brute-force route's chunk cull) is
+// conservative except for lines lying within ~17 u |o - v0| of a triangle's plane and within ~17 u rho / K of
+// parallel to it (tests/native/cull_diff.cpp constructs such lines); the "cluster_cull" knob = 0 removes the cull.
 struct CullMargin {
   float K;          // the box-only tests' coefficient (DevScene::cl_margin)
   float K_lo;       // the slab level's floor (cl_margin_lo)

@@ -151,8 +151,12 @@ struct DevScene {
   // cl_mask[b * num_clusters + c] = the danger mask over the cluster's 64 entries (bucket-major: a ray's
   // pairs, consecutive clusters of one leaf in one bucket, share cache lines); null: the fast-margin cull
   // (tuning "cull_exact" = 0) or no one-level cull at all
-  const unsigned long long* cl_mask;  // [num_clusters][6 mask_n^2] danger masks
+  const unsigned long long* cl_mask;  // [6 mask_n^2][num_clusters] danger masks
   int mask_n;                          // cube-map cells per face edge (dir_bucket)
+  // ... and per (bucket, cluster), in the same order, the code of a bound on the rigorous coefficients of the
+  // mask's triangles (mask_bound_code: 0 = the mask is never needed); null: every missed pair reads its mask
+  // (tuning "cull_bound" = 0)
+  const unsigned char* cl_mq;
   // per cluster entry: the triangle's unit normal (float) and 17.5 u rho (the exact cull's per-triangle
   // bound); w = -1: never passes (padding, small degenerate), w = +inf: may pass for any direction
   const float4* cl_tn;
@@ -582,10 +586,18 @@ KDPT_HD bool cluster_may_pass_obb(float4 lo, float4 hi, float4 n, float4 u, floa
 // whose bound holds it.  Any finite nonzero d works (the cull only runs for lanes whose 1 / d components are
 // all finite).
 // 1 / x for box_miss and dir_bucket: the hardware reciprocal (1 ulp) on the device, the division on the host;
-// box_miss's 1e-5 slack and the masks' 1e-5 cell growth cover either
+// box_miss's 1e-5 slack and the masks' 1e-5 cell growth cover either.  A float within 1 ulp of 1 / x is the
+// rounded quotient or one of its two neighbours: the cull harness (tests/native/cull_diff.cpp, KDPT_RCP_ULP)
+// evaluates every line with each of the three.
+#if !defined(__HIP_DEVICE_COMPILE__) && defined(KDPT_RCP_ULP)
+extern thread_local int kdpt_rcp_ulp;  // -1, 0, +1: the host quotient moved by that many ulps
+#endif
 KDPT_HD float kd_rcp(float x) {
 #if defined(__HIP_DEVICE_COMPILE__)
   return __builtin_amdgcn_rcpf(x);
+#elif defined(KDPT_RCP_ULP)
+  const float r = 1.0f / x;
+  return kdpt_rcp_ulp == 0 ? r : std::nextafter(r, kdpt_rcp_ulp > 0 ? HUGE_VALF : -HUGE_VALF);
 #else
   return 1.0f / x;
 #endif
@@ -657,21 +669,45 @@ KDPT_HD bool danger_needs_test(float4 tn, f3 d, float D, float c) {
   return !(g > 0.0f) || tn.w * 1.00001f >= (D - c) * g;
 }
 
-// The per-cluster exact margin (kdpt_clusters.h, ClusterSet::kc = {chord_eff, a, K_rig, c}) for a line of
-// direction d, nd = n . d with n the cluster's slab normal.  glm's test is single-sided: its float determinant
-// a_t = fl(e1 . (d x e2)) must reach FLT_EPSILON, and a_t is within 5.8 u |e1||e2| of -|N_t| (N_t / |N_t|) . d.
-// Every unit normal of the cluster lies within its chord of n, and chord_eff = chord (1 + 8u) + 5.8 u rho + 32 u
-// (rho: the cluster's largest |e1||e2| / |N_t|) also covers nd's rounding, so
-//   nd >  chord_eff: every a_t < 0 -- no triangle of the cluster passes: cull (returns -1);
-//   g = -nd - chord_eff > 0: a_t >= |N_t| g, so a passing point lies within 17.5 u rho / g |s| + c of the line
-//     ("Cluster cull"): K = a / g + c, at most K_rig;
-//   otherwise (a line within the chord of the cluster's patch plane): the direction-free K_rig = 8.75 E + c.
-// The floor K_lo only widens the box.
-KDPT_HD float cull_k_exact(float nd, float4 kc, float K_lo) {
-  if (nd > kc.x) return -1.0f;
-  const float g = -nd - kc.x;
-  const float K = g > 0.0f ? fminf(kc.z, kc.y / g + kc.w) : kc.z;
-  return fmaxf(K, K_lo);
+// The bound codes of the masked cull (DevScene::cl_mq).  Every triangle t has a direction-free rigorous
+// coefficient K_t = 8.75 |e1||e2| + c ("Cluster cull": a line glm's float u/v tests accept for t
+// passes within K_t W of any region holding t), so a (line, cluster) pair whose line misses the cluster's box at
+// the largest K_t of the mask's triangles needs none of them.  Code q in 1 .. 254 stands for the exact float
+// mask_bound(q) = (17 + q % 16) 2^(q / 16 - 14) (1.1e-3 .. 64, steps of at most 1/17); 0: the mask is empty (or
+// each of its K_t is at most the box coefficient Kf, which the pair already missed); 255: no bound.  The same
+// float on the host and on gfx950 (ldexp is exact), so the encoder's comparisons hold on both.
+KDPT_HD float mask_bound(uint32_t q) { return ldexpf((float)(17u + (q & 15u)), (int)(q >> 4) - 14); }
+KDPT_HD uint32_t mask_bound_code(float Kb, float Kf) {
+  if (Kb <= Kf) return 0u;
+  uint32_t lo = 1u, hi = 255u;  // the smallest q in 1 .. 254 with mask_bound(q) >= Kb; 255 if none (or NaN)
+  while (lo < hi) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (mask_bound(mid) >= Kb) hi = mid;
+    else lo = mid + 1u;
+  }
+  return lo;
+}
+
+// One (bucket, cluster) cell of the masked cull (kdpt_clusters.h build_dir_masks on the host and k_build_masks on
+// the device run this same code, -ffp-contract=off, so both give the same bits).  Per entry k of the cluster: its
+// unit normal n_k, beta_k and dthr_k (kdpt_clusters.h mask_entries) and its rigorous coefficient krig_k; the
+// bucket: its centre direction D[0..2] and radius D[3].  Entry k is in the danger mask when some direction of the
+// bucket makes it front-facing (n_k . d <= beta_k) and needing more than Kf (n_k . d >= dthr_k), and K_t > Kf
+// (otherwise the missed box test at Kf already covers it); the code bounds the krig of the mask's entries.
+KDPT_HD void dir_mask_cell(const double* nx, const double* ny, const double* nz, const double* beta,
+                           const double* dthr, const float* krig, const double* D, float Kf,
+                           unsigned long long& mask, uint32_t& code) {
+  unsigned long long md = 0ull;
+  float kb = 0.0f;
+  for (int k = 0; k < 64; k++) {
+    const double x = nx[k] * D[0] + ny[k] * D[1] + nz[k] * D[2];
+    if (x - D[3] <= beta[k] && x + D[3] >= dthr[k] && krig[k] > Kf) {
+      md |= 1ull << k;
+      kb = krig[k] > kb ? krig[k] : kb;
+    }
+  }
+  mask = md;
+  code = md ? mask_bound_code(kb, Kf) : 0u;
 }
 
 #if defined(__HIPCC__) || defined(__HIP__)
@@ -1530,8 +1566,9 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       // With direction masks (S.cl_mask: the exact cull, DESIGN.md 4 "Cluster cull") a miss may still hide a
       // u/v pass of a triangle nearly parallel to the line: the cluster's danger mask for the ray's direction
       // bucket (kdpt_clusters.h build_dir_masks) lists every triangle that can need more than cl_margin for
-      // some direction of the bucket.  The mask is requested with the box test and read after the pass's
-      // sweeps (its latency hidden behind them); the missed pair's lane then walks its bits, deciding each
+      // some direction of the bucket.  The cell's bound code (S.cl_mq, one byte, requested with the box test)
+      // says whether the mask can matter for this line at all; only then is the mask requested, before the
+      // pass's sweeps, and read after them (its latency hidden behind them); the lane then walks its bits, deciding each
       // triangle from its unit normal and the line's box_miss distance (danger_needs_test), and the rare one
       // that needs it gets glm's u/v tests.  A pass sweeps the whole cluster late, as the uncull'd walk would
       // have: the sweep's results fold by max / min / sum, so a late sweep is the same as an early one.
@@ -1558,10 +1595,13 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
           const f3 oo = mk3(od.x, od.y, od.z), dd = mk3(od.w, d2.x, d2.y);
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
           float4 clo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), chi = clo;
-          unsigned long long dm = 0ull;
+          uint32_t mi = 0u, q = 0u;  // the pair's (bucket, cluster) cell and its bound code (exact cull)
           const bool valid = hit;
           if (valid) {
-            if (exact) dm = S.cl_mask[(size_t)dir_bucket(dd, S.mask_n) * S.num_clusters + c];
+            if (exact) {
+              mi = (uint32_t)dir_bucket(dd, S.mask_n) * (uint32_t)S.num_clusters + (uint32_t)c;
+              q = S.cl_mq ? (uint32_t)S.cl_mq[mi] : 255u;
+            }
             clo = clusters.lo_of(c);
             chi = clusters.hi_of(c);
             hit = cluster_may_pass(clo, chi, oo, ii, S.cl_margin);
@@ -1574,7 +1614,12 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
                                            cn.x * dd.x + cn.y * dd.y + cn.z * dd.z, S.cl_margin);
             }
           }
-          if (exact && valid && !hit) m = dm;
+          // a missed pair reads its danger mask only when its line also meets the cluster's box widened by
+          // the mask's bound (the mask's triangles' largest rigorous coefficient, mask_bound): most cells are
+          // empty or far, and skip the 8-byte load from the large table
+          if (exact && valid && !hit && q != 0u &&
+              (q == 255u || cluster_may_pass(clo, chi, oo, ii, mask_bound(q))))
+            m = S.cl_mask[mi];
         }
         if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
         sweep(hit, c, own);

@@ -16,6 +16,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cfloat>
 #include <cmath>
 #include <cstdio>
@@ -45,6 +46,7 @@ constexpr int TILE = 256;  // paths per workgroup (4 waves of 64)
 constexpr int MAX_KEYS = 64;
 
 thread_local std::string g_last_error;
+double g_reduce_spin_us = 0;  // kdpt_set_tuning(NULL, "reduce_spin_us", v): the default of new contexts
 
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -1695,9 +1697,12 @@ struct kdpt_ctx {
   // the exact one-level cull's direction masks (kdpt_clusters.h build_dir_masks), built when the scene's rigorous
   // margin is above the cap; S.cl_mask points at them unless a knob chose another cull
   unsigned long long* mask_dev = nullptr;
+  unsigned char* mq_dev = nullptr;  // their bound codes (DevScene::cl_mq)
   float4* tn_dev = nullptr;  // the clusters' per-entry normal records (DevScene::cl_tn)
   int mask_n = 0;
   bool cull_exact = true;   // "cull_exact" knob: 0 = the fast-margin cull (not exact for such scenes)
+  bool cull_bound = true;   // "cull_bound" knob: 0 = every missed pair reads its mask (no bound codes)
+  double create_ms = 0, mask_build_ms = 0;  // kdpt_create's host wall time, and the masks' (kdpt_stats)
   bool cull_scene = true;   // false after "cluster_cull" = 0 or a fixed "cull_margin"
   std::unique_ptr<ClusterSet> mask_cs;  // the clusters the masks were built from ("cull_mask_n" rebuilds)
   int tree_format = 0;             // "tree_format" knob: 16 / 32 = LDS node records of that size only
@@ -1765,6 +1770,7 @@ struct kdpt_ctx {
   hipEvent_t frame_ev[2] = {nullptr, nullptr};      // frame_buf[k] consumed by its reduce
   hipEvent_t frame_acc_ev[2] = {nullptr, nullptr};  // frame_buf[k]'s accumulations done
   hipStream_t reduce_stream = nullptr;  // the frames' reduces and image adds, beside the accumulation stream
+  double reduce_spin_us = 0;  // "reduce_spin_us" knob: a device spin before every frame's reduce (a slow peer)
   std::vector<void*> host_reg;  // pageable host `out` ranges pinned for kdpt_render_frames (released at synchronize)
 };
 
@@ -1978,28 +1984,110 @@ void fix_cull(kdpt_ctx* c, float K) {
 // margins in place, else the margin-only cull.
 void apply_cull_route(kdpt_ctx* c) {
   c->S.cl_mask = (c->mask_dev && c->cull_exact && c->cull_scene) ? c->mask_dev : nullptr;
+  c->S.cl_mq = (c->S.cl_mask && c->cull_bound) ? c->mq_dev : nullptr;
   c->S.mask_n = c->mask_n;
   c->S.cl_tn = c->tn_dev;
 }
-// The direction masks of the scene's clusters at resolution n (cube-map cells per face edge), uploaded.
+// The masked cull's cells on the device (kdpt_device.h dir_mask_cell, the code the host builder runs): one
+// workgroup per (cluster, 256 buckets), the cluster's 64 entries staged in LDS (every lane reads the same entry:
+// a broadcast), one mask and one bound code per lane, written bucket-major.
+__global__ void __launch_bounds__(256) k_build_masks(const double* __restrict__ ent, const float* __restrict__ krig,
+                                                     const double* __restrict__ bd, int ncl, int nb, float Kf,
+                                                     unsigned long long* __restrict__ masks,
+                                                     unsigned char* __restrict__ codes) {
+  __shared__ double se[5][64];
+  __shared__ float sk[64];
+  const int c = blockIdx.x;
+  const size_t ne = 64 * (size_t)ncl;
+  if (threadIdx.x < 64) {
+    for (int f = 0; f < 5; f++) se[f][threadIdx.x] = ent[f * ne + 64 * (size_t)c + threadIdx.x];
+    sk[threadIdx.x] = krig[64 * (size_t)c + threadIdx.x];
+  }
+  __syncthreads();
+  const int b = blockIdx.y * 256 + threadIdx.x;
+  if (b >= nb) return;
+  unsigned long long m;
+  uint32_t q;
+  dir_mask_cell(se[0], se[1], se[2], se[3], se[4], sk, bd + 4 * (size_t)b, Kf, m, q);
+  masks[(size_t)b * ncl + c] = m;
+  codes[(size_t)b * ncl + c] = (unsigned char)q;
+}
+
+// Release one of the context's device allocations before kdpt_destroy (a rebuilt table).
+void dfree(kdpt_ctx* c, void* p) {
+  if (!p) return;
+  auto it = std::find(c->allocs.begin(), c->allocs.end(), p);
+  if (it != c->allocs.end()) c->allocs.erase(it);
+  (void)hipFree(p);
+}
+
+// The direction masks of the scene's clusters at resolution n (cube-map cells per face edge) and their bound
+// codes, built on the device (k_build_masks) from the per-entry records and the bucket directions the host
+// computes (kdpt_clusters.h mask_entries / mask_buckets; tests/test_gpu_parity.py checks the cells against the
+// host builder).  A rebuild (knobs "cull_mask_n", "cull_fast_k") frees the previous tables.
 int build_masks(kdpt_ctx* c, int n) {
-  std::vector<unsigned long long> cm;
-  build_dir_masks(*c->mask_cs, n, c->cull.K, cm);
-  // bucket-major on the device (DevScene::cl_mask)
-  const size_t ncl = c->mask_cs->info.size(), nb = 6 * (size_t)n * n;
-  std::vector<unsigned long long> m(cm.size());
-  for (size_t k = 0; k < ncl; k++)
-    for (size_t b = 0; b < nb; b++) m[b * ncl + k] = cm[k * nb + b];
-  unsigned long long* d = nullptr;
-  int rc = dupload(c, &d, m.data(), m.size());
-  if (rc) return rc;
+  const auto t0 = std::chrono::steady_clock::now();
+  const ClusterSet& cs = *c->mask_cs;
+  const int ncl = (int)cs.info.size(), nb = 6 * n * n;
+  const float Kf = c->cull.K;
+  MaskEntries me;
+  mask_entries(cs, Kf, me);
+  std::vector<double> bd;
+  mask_buckets(n, bd);
+  const size_t ne = 64 * (size_t)ncl;
+  std::vector<double> ent(5 * ne);
+  for (size_t k = 0; k < ne; k++) {
+    ent[k] = me.nx[k];
+    ent[ne + k] = me.ny[k];
+    ent[2 * ne + k] = me.nz[k];
+    ent[3 * ne + k] = me.beta[k];
+    ent[4 * ne + k] = me.dthr[k];
+  }
+  dfree(c, c->mask_dev);
+  dfree(c, c->mq_dev);
+  c->mask_dev = nullptr;
+  c->mq_dev = nullptr;
+  c->S.cl_mask = nullptr;
+  c->S.cl_mq = nullptr;
+  unsigned long long* dm = nullptr;
+  unsigned char* dq = nullptr;
+  int rc;
+  if ((rc = dalloc(c, &dm, (size_t)nb * ncl)) || (rc = dalloc(c, &dq, (size_t)nb * ncl))) return rc;
+  c->mask_dev = dm;
+  c->mq_dev = dq;
+  double* d_ent = nullptr;
+  float* d_krig = nullptr;
+  double* d_bd = nullptr;
+  auto release = [&]() {
+    (void)hipFree(d_ent);
+    (void)hipFree(d_krig);
+    (void)hipFree(d_bd);
+  };
+  // (the uploads on the context's stream, ahead of the kernel; pageable sources are staged before each call
+  // returns, and the stream is drained before the temporaries go)
+  if (hipMalloc(&d_ent, ent.size() * sizeof(double)) != hipSuccess ||
+      hipMalloc(&d_krig, me.krig.size() * sizeof(float)) != hipSuccess ||
+      hipMalloc(&d_bd, bd.size() * sizeof(double)) != hipSuccess ||
+      hipMemcpyAsync(d_ent, ent.data(), ent.size() * sizeof(double), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+      hipMemcpyAsync(d_krig, me.krig.data(), me.krig.size() * sizeof(float), hipMemcpyHostToDevice, c->stream) !=
+          hipSuccess ||
+      hipMemcpyAsync(d_bd, bd.data(), bd.size() * sizeof(double), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+    (void)hipStreamSynchronize(c->stream);
+    release();
+    return fail(KDPT_ERR_HIP, "mask build: device buffers");
+  }
+  hipLaunchKernelGGL(k_build_masks, dim3(ncl, (nb + 255) / 256), dim3(256), 0, c->stream, d_ent, d_krig, d_bd, ncl,
+                     nb, Kf, dm, dq);
+  const hipError_t e1 = hipGetLastError(), e2 = hipStreamSynchronize(c->stream);
+  release();
+  if (e1 != hipSuccess || e2 != hipSuccess) return fail(KDPT_ERR_HIP, "k_build_masks failed");
   if (!c->tn_dev) {
     std::vector<float4> tn;
-    build_entry_normals(*c->mask_cs, tn);
+    build_entry_normals(cs, tn);
     if ((rc = dupload(c, &c->tn_dev, tn.data(), tn.size()))) return rc;
   }
-  c->mask_dev = d;
   c->mask_n = n;
+  c->mask_build_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
   apply_cull_route(c);
   return KDPT_OK;
 }
@@ -2275,6 +2363,7 @@ void kdpt_default_options(kdpt_options* o) {
 const char* kdpt_last_error(void) { return g_last_error.c_str(); }
 
 int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_ctx** out) {
+  const auto t_create = std::chrono::steady_clock::now();
   if (!sc || !out) return fail(KDPT_ERR_ARG, "null scene/out");
   *out = nullptr;
   kdpt_options o;
@@ -2591,6 +2680,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   // the scene's uploads (hipMemcpy) complete before any kernel of the context's non-blocking streams
   HIP_TRY(hipDeviceSynchronize());
   if ((rc = kdpt_reset(c))) return bail(rc);
+  c->reduce_spin_us = g_reduce_spin_us;
+  c->create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_create).count();
   *out = c;
   return KDPT_OK;
 }
@@ -2627,6 +2718,11 @@ int kdpt_set_options(kdpt_ctx* c, const kdpt_options* o) {
 }
 
 int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
+  if (!c && name && std::string(name) == "reduce_spin_us") {  // the process default of contexts created later
+    if (!(value >= 0.0 && value <= 1e6)) return fail(KDPT_ERR_ARG, "reduce_spin_us must be in [0, 1e6]");
+    g_reduce_spin_us = value;
+    return KDPT_OK;
+  }
   if (!c || !name) return fail(KDPT_ERR_ARG, "null arg");
   if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
   HIP_TRY(hipSetDevice(c->device));
@@ -2683,7 +2779,7 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     if (rc) return rc;
     if (c->grid_env) c->trace_grid = std::max(1, (int)(c->full_trace_grid * frac));
   } else if (k == "cluster_cull" || k == "cull_margin" || k == "cull_exact" || k == "cull_mask_n" ||
-             k == "cull_fast_k") {
+             k == "cull_fast_k" || k == "cull_bound") {
     if (k == "cluster_cull") {
       // 0: no cluster / chunk cull at all (every big-leaf cluster swept: exact by construction, whatever the
       // scene's margin); 1: the scene's margins (and masks)
@@ -2699,6 +2795,10 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     } else if (k == "cull_exact") {
       // 0: the fast-margin one-level cull instead of the masked exact one (A/B; not exact for such scenes)
       c->cull_exact = v != 0;
+    } else if (k == "cull_bound") {
+      // 0: the masked cull reads every missed pair's mask instead of first checking its cell's bound code (A/B;
+      // exact either way)
+      c->cull_bound = v != 0;
     } else if (k == "cull_fast_k") {
       // the masked cull's box coefficient (default CULL_MARGIN_MASKED), its direction masks rebuilt for it: a
       // wider box sweeps more clusters, a narrower one leaves more danger triangles to decide
@@ -2724,7 +2824,9 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     c->profile_steps = v >= 2;
   } else if (k == "sync_debug") {
     c->sync_debug = v != 0;
-
+  } else if (k == "reduce_spin_us") {
+    if (!(value >= 0.0 && value <= 1e6)) return fail(KDPT_ERR_ARG, "reduce_spin_us must be in [0, 1e6]");
+    c->reduce_spin_us = value;
   } else {
     return fail(KDPT_ERR_ARG, "unknown tuning knob " + k);
   }
@@ -3014,6 +3116,21 @@ int kdpt_save_hdr(kdpt_ctx* c, const char* path, float samples) {
   return rc ? fail(rc, std::string("cannot write ") + path) : KDPT_OK;
 }
 
+int kdpt_cull_masks(kdpt_ctx* c, int* mask_n, int* num_clusters, unsigned long long* masks, uint8_t* codes) {
+  if (!c || !mask_n || !num_clusters) return fail(KDPT_ERR_ARG, "null arg");
+  HIP_TRY(hipSetDevice(c->device));
+  *mask_n = c->mask_dev ? c->mask_n : 0;
+  *num_clusters = c->S.num_clusters;
+  if (!c->mask_dev) return KDPT_OK;
+  const size_t cells = 6 * (size_t)c->mask_n * c->mask_n * (size_t)c->S.num_clusters;
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  if (masks)
+    HIP_TRY(hipMemcpyAsync(masks, c->mask_dev, cells * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
+  if (codes) HIP_TRY(hipMemcpyAsync(codes, c->mq_dev, cells, hipMemcpyDeviceToHost, c->stream));
+  HIP_TRY(hipStreamSynchronize(c->stream));
+  return KDPT_OK;
+}
+
 int kdpt_get_stats(kdpt_ctx* c, kdpt_stats* st) {
   if (!c || !st) return fail(KDPT_ERR_ARG, "null arg");
   HIP_TRY(hipSetDevice(c->device));
@@ -3027,6 +3144,8 @@ int kdpt_get_stats(kdpt_ctx* c, kdpt_stats* st) {
   c->stats.total_segments = (long long)tot;
   c->stats.intersect_ms_total = c->intersect_ms_total;
   c->stats.intersect_launches_total = c->intersect_launches_total;
+  c->stats.create_ms = c->create_ms;
+  c->stats.mask_build_ms = c->mask_build_ms;
   *st = c->stats;
   return KDPT_OK;
 }
@@ -3623,6 +3742,22 @@ __global__ void k_sum_frames(float* __restrict__ out, FrameParts parts, int n3) 
   out[i] = v;
 }
 
+// Diagnostic ("reduce_spin_us" knob): one wave that spins for `ticks` of the device's constant-rate clock on the
+// reduce stream ahead of a frame's reduce -- what an ncclReduce waiting for a slower peer looks like to this
+// GPU's queues (tools/reduce_spin_probe.py).
+__global__ void k_spin(unsigned long long ticks) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(16);
+}
+
+int reduce_spin(kdpt_ctx* c, hipStream_t st) {
+  if (!(c->reduce_spin_us > 0)) return KDPT_OK;
+  const unsigned long long ticks = (unsigned long long)(c->reduce_spin_us * c->wall_khz / 1000.0);
+  hipLaunchKernelGGL(k_spin, dim3(1), dim3(64), 0, st, ticks);
+  HIP_TRY(hipGetLastError());
+  return KDPT_OK;
+}
+
 void release_comm(kdpt_ctx* c) {
   const Rccl* R = c->comm && c->owns_comm ? rccl() : nullptr;
   if (R) (void)R->commDestroy((ncclComm_t)c->comm);
@@ -3767,6 +3902,7 @@ int kdpt_render_frames(kdpt_ctx* c, int first_frame, int frames, int spp, int pi
     const hipStream_t rs = c->reduce_stream;
     HIP_TRY(hipEventRecord(c->frame_acc_ev[f & 1], c->accum_stream));
     HIP_TRY(hipStreamWaitEvent(rs, c->frame_acc_ev[f & 1], 0));
+    if ((rc = reduce_spin(c, rs))) return rc;
     const float* sum = fb;
     if (c->external_reduce) {  // the caller reduces: every rank's share goes out as it is
       if (out) HIP_TRY(hipMemcpyAsync(out + (size_t)k * n3, fb, sizeof(float) * n3, hipMemcpyDefault, rs));
@@ -3851,6 +3987,7 @@ int kdpt_render_sharded(const kdpt_scene* scene, const kdpt_options* opt, int nd
       if (hipEventRecord(ci->frame_acc_ev[f & 1], ci->accum_stream) != hipSuccess ||
           hipStreamWaitEvent(ci->reduce_stream, ci->frame_acc_ev[f & 1], 0) != hipSuccess)
         return cleanup(fail(KDPT_ERR_HIP, "frame events"));
+      if ((rc = reduce_spin(ci, ci->reduce_stream))) return cleanup(rc);
     }
     if (hipSetDevice(c0->device) != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "hipSetDevice"));
     if ((rc = frame_buffers(c0))) return cleanup(rc);

@@ -90,7 +90,7 @@ class Stats(C.Structure):
                 ("total_segments", C.c_longlong), ("intersect_ms_total", C.c_double),
                 ("intersect_launches_total", C.c_longlong), ("intersect_device_ms_total", C.c_double),
                 ("intersect_device_launches_total", C.c_longlong), ("intersect_grid_share", C.c_float),
-                ("total_trace_rays", C.c_longlong)]
+                ("total_trace_rays", C.c_longlong), ("create_ms", C.c_double), ("mask_build_ms", C.c_double)]
 
 
 class SceneDesc(C.Structure):
@@ -115,7 +115,7 @@ EXPORTS = [
     "kdpt_write_hdr", "kdpt_free", "kdpt_set_tuning", "kdpt_selftest_glm", "kdpt_set_options", "kdpt_scene_build_device",
     "kdpt_scene_kd_build_ms", "kdpt_build_kd_device", "kdpt_scene_load_device", "kdpt_trace_config",
     "kdpt_cull_margin", "kdpt_comm_unique_id", "kdpt_comm_init", "kdpt_render_frames", "kdpt_render_sharded",
-    "kdpt_comm_library",
+    "kdpt_comm_library", "kdpt_cull_masks",
 ]
 
 REDUCE_RCCL, REDUCE_COPY = 0, 1  # kdpt_render_sharded's reduce (KDPT_REDUCE_*)
@@ -162,6 +162,8 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     lib.kdpt_trace_config.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), P(C.c_int), P(C.c_longlong)]
     if hasattr(lib, "kdpt_cull_margin"):  # absent from older builds used in A/B runs
         lib.kdpt_cull_margin.argtypes = [C.c_void_p, P(C.c_float), P(C.c_double), P(C.c_int)]
+    if hasattr(lib, "kdpt_cull_masks"):
+        lib.kdpt_cull_masks.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), C.c_void_p, C.c_void_p]
     if hasattr(lib, "kdpt_render_frames"):
         lib.kdpt_comm_unique_id.argtypes = [C.c_void_p]
         lib.kdpt_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
@@ -517,6 +519,20 @@ class PathTracer:
         k, r, e = C.c_float(), C.c_double(), C.c_int()
         _check(self.lib.kdpt_cull_margin(self._ctx, C.byref(k), C.byref(r), C.byref(e)), "kdpt_cull_margin")
         return {"cull_margin": k.value, "cull_rigorous": r.value, "cull_exact": bool(e.value)}
+
+    def cull_masks(self):
+        """kdpt_cull_masks: (mask_n, masks, codes) of the masked cull as the device built them, bucket-major arrays
+        of shape [6 mask_n^2, num_clusters]; (0, None, None) when the scene has none."""
+        n, ncl = C.c_int(), C.c_int()
+        _check(self.lib.kdpt_cull_masks(self._ctx, C.byref(n), C.byref(ncl), None, None), "kdpt_cull_masks")
+        if n.value == 0:
+            return 0, None, None
+        cells = (6 * n.value * n.value, ncl.value)
+        masks = np.zeros(cells, np.uint64)
+        codes = np.zeros(cells, np.uint8)
+        _check(self.lib.kdpt_cull_masks(self._ctx, C.byref(n), C.byref(ncl), masks.ctypes.data, codes.ctypes.data),
+               "kdpt_cull_masks")
+        return n.value, masks, codes
 
     def trace_grid_share(self) -> float:
         return float(self.stats().intersect_grid_share)

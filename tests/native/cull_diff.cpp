@@ -18,6 +18,7 @@
 #include <random>
 #include <vector>
 
+#define KDPT_RCP_ULP  // kd_rcp follows kdpt_rcp_ulp (the device reciprocal's 1-ulp error)
 #include "../../kdtreepathtraceroptimization_amd/csrc/kdpt_clusters.h"
 
 // the masked cull's box coefficient and mask resolution: the product's (cluster_margin, dir_mask_resolution)
@@ -26,6 +27,10 @@ static float mask_kf() { return getenv("MASK_KF") ? (float)atof(getenv("MASK_KF"
 static int mask_res(int ncl) { return getenv("MASK_N") ? atoi(getenv("MASK_N")) : kdpt::dir_mask_resolution(ncl); }
 
 using namespace kdpt;
+
+namespace kdpt {
+thread_local int kdpt_rcp_ulp = 0;  // kd_rcp's perturbation (KDPT_RCP_ULP): the lines are checked at -1, 0, +1
+}
 
 namespace {
 
@@ -180,11 +185,70 @@ double bound_ratio(f3 o, f3 d, float4 v0, float4 e1, float4 e2, float bx, float 
   return (double)(std::sqrt(dist2) / bound);
 }
 
+// The product's masked cull (kdpt_device.h trace_phase, one-level route) for a (line, cluster) pair whose line
+// missed the cluster's fast-margin box or oriented box: the pair's cell (dir_bucket) and its bound code; when
+// the line meets the box widened by mask_bound(code) (or the kernel reads every mask: knob "cull_bound" = 0), the
+// danger mask's triangles that danger_needs_test keeps (those get glm's u/v tests).  `loaded`: the pair's 8-byte
+// mask was read.
+struct MaskTables {
+  int n = 0, ncl = 0;
+  float c = 0.0f;
+  std::vector<unsigned long long> masks;  // bucket-major, DevScene::cl_mask
+  std::vector<unsigned char> codes;       // DevScene::cl_mq
+  std::vector<float4> tn;                 // DevScene::cl_tn
+  void build(const ClusterSet& cs, int res, float Kf, float cc) {
+    n = res;
+    ncl = (int)cs.info.size();
+    c = cc;
+    build_dir_masks(cs, n, Kf, masks, codes);
+    build_entry_normals(cs, tn);
+  }
+  // bound: the kernel's "cull_bound" route (the cell's code checked before the mask is read)
+  unsigned long long needs(bool bound, int cl, float4 L, float4 H, f3 o, f3 inv, f3 d, bool& loaded,
+                           int& items) const {
+    const uint32_t mi = (uint32_t)dir_bucket(d, n) * (uint32_t)ncl + (uint32_t)cl;
+    const uint32_t q = bound ? codes[mi] : 255u;
+    loaded = q != 0u && (q == 255u || cluster_may_pass(L, H, o, inv, mask_bound(q)));
+    items = 0;
+    if (!loaded) return 0ull;
+    unsigned long long m = masks[mi], nm = 0ull;
+    const float D = box_miss(L, H, o, inv);
+    while (m) {
+      const int k = __builtin_ctzll(m);
+      m &= m - 1;
+      items++;
+      if (danger_needs_test(tn[64 * (size_t)cl + k], d, D, c)) nm |= 1ull << k;
+    }
+    return nm;
+  }
+  // the same with kd_rcp's quotient moved by -1, 0 and +1 ulp (v_rcp_f32's error), and with and without the
+  // bound codes: the triangles kept under every one of them (a pass must be kept under each); stats from the
+  // unperturbed product route
+  unsigned long long needs_all(bool bound, int cl, float4 L, float4 H, f3 o, f3 inv, f3 d, bool& loaded,
+                               int& items) const {
+    unsigned long long all = ~0ull;
+    for (int bnd : {1, 0})
+      for (int p : {0, -1, 1}) {
+        kdpt_rcp_ulp = p;
+        bool ld;
+        int it;
+        all &= needs(bnd != 0, cl, L, H, o, inv, d, ld, it);
+        if (p == 0 && (bnd != 0) == bound) {
+          loaded = ld;
+          items = it;
+        }
+      }
+    kdpt_rcp_ulp = 0;
+    return all;
+  }
+};
+
 // Cull statistics of real rays through the traversal (--sim): each ray walks the tree (traverseKD, compiled
-// here for the host); for every big leaf it tests, every cluster of the leaf is evaluated with the scene-wide
-// cull the kernels ran up to round 4 (box at the scene margin + oriented box at cull_margin_dir) and with the
-// per-cluster exact cull (cull_k_exact: back-facing clusters dropped, the box and the oriented box at the
-// cluster's own margin).  A pair either cull drops while a triangle passes glm's u/v tests is a violation.
+// here for the host); for every big leaf it tests, every cluster of the leaf is evaluated with the fast cull (box
+// at the scene margin + oriented box at cull_margin_dir) and with the product's masked cull (box and oriented
+// box at the masked cull's coefficient Kf; a missed pair's bound code, mask and danger_needs_test, under each
+// of the three reciprocal perturbations).  A pair a cull drops while a triangle passes glm's u/v tests, or a
+// passing triangle the masked cull does not test, is a violation.
 int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_bare* tris, int nt,
         const std::vector<float4>& tv, const std::vector<float4>& e1, const std::vector<float4>& e2,
         const ClusterGrouping& grp) {
@@ -223,20 +287,13 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
   S.obj_material_offsets = offs.data();
   S.n0_left = nodes[0].leftID; S.n0_right = nodes[0].rightID;
   S.n1_left = nn > 1 ? nodes[1].leftID : -1; S.n1_right = nn > 1 ? nodes[1].rightID : -1;
-  long long leaves = 0, pairs = 0, old_sw = 0, new_sw = 0, prod = 0, back = 0, front = 0, graze = 0, viol_old = 0,
-            viol_new = 0, nofast = 0, small_tris = 0, old_tris = 0, new_tris = 0, graze_tris = 0, ref_susp = 0,
-            ref_items = 0, ref_back = 0, ref_sw = 0, ref_tris = 0, refq_sw = 0, viol_ref = 0, cmp_rounds = 0,
-            cmp_items = 0, viol_cmp = 0, msk_items = 0, msk_pairs = 0, viol_msk = 0, msk_needed = 0, t2_near = 0,
-            t2_items = 0, viol_t2 = 0;
-  const int mask_n = mask_res((int)cs.info.size());
+  long long leaves = 0, pairs = 0, old_sw = 0, msk_sw = 0, prod = 0, viol_old = 0, nofast = 0, small_tris = 0,
+            old_tris = 0, msk_missed = 0, msk_loads = 0, msk_items = 0, viol_msk = 0, msk_needed = 0;
   const float KF = mask_kf();
-  const float KD = getenv("MASK_KD") ? (float)atof(getenv("MASK_KD")) : 1e-3f;
-  std::vector<unsigned long long> masks, masks2;
-  build_dir_masks(cs, mask_n, KF, masks);
-  build_dir_masks(cs, mask_n, KD, masks2);
-  std::vector<float4> tn;
-  build_entry_normals(cs, tn);
-#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, pairs, old_sw, new_sw, prod, back, front, graze, viol_old, viol_new, nofast, small_tris, old_tris, new_tris, graze_tris, ref_susp, ref_items, ref_back, ref_sw, ref_tris, refq_sw, viol_ref, cmp_rounds, cmp_items, viol_cmp, msk_items, msk_pairs, viol_msk, msk_needed, t2_near, t2_items, viol_t2)
+  const bool bound = !getenv("MASK_BOUND") || atoi(getenv("MASK_BOUND")) != 0;  // stats of that route
+  MaskTables mt;
+  mt.build(cs, mask_res((int)cs.info.size()), KF, cm.c);
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, pairs, old_sw, msk_sw, prod, viol_old, nofast, small_tris, old_tris, msk_missed, msk_loads, msk_items, viol_msk, msk_needed)
   for (long long i = 0; i < nr; i++) {
     const f3 o = mk3(r[6 * i], r[6 * i + 1], r[6 * i + 2]), d = mk3(r[6 * i + 3], r[6 * i + 4], r[6 * i + 5]);
     const f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -262,166 +319,50 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
       for (int c = lc.x; c < lc.x + lc.y; c++) {
         pairs++;
         const int2 inf = cs.info[c];
-        bool pass = false;
-        for (int k = 0; k < inf.y && !pass; k++) {
+        unsigned long long passes = 0ull;  // the cluster's triangles that pass glm's u/v tests
+        for (int k = 0; k < inf.y; k++) {
           float bx, by, bz;
-          pass = tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, o, d, bx, by, bz) >= 1;
+          if (tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, o, d, bx, by, bz) >= 1)
+            passes |= 1ull << k;
         }
-        prod += pass;
+        prod += passes != 0ull;
         if (!fast) {
           old_sw++;
-          new_sw++;
+          msk_sw++;
           continue;
         }
         const float4 L = cs.lo[c], H = cs.hi[c], n = cs.nrm[c];
         const bool ok_old = cluster_may_pass(L, H, o, inv, cm.K) &&
                             cluster_may_pass_obb(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ck);
-        const float ndv = n.x * d.x + n.y * d.y + n.z * d.z;
-        const float K = cull_k_exact(ndv, cs.kc[c], KF);
-        if (K < 0) back++;
-        else if (-ndv - cs.kc[c].x > 0.0f) front++;
-        else graze++;
-        const bool ok_new = K >= 0 && cluster_may_pass(L, H, o, inv, K) &&
-                            cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, K);
-        // the refined exact cull: a fast-culled pair whose cone gives no bound is resolved per triangle (its
-        // unit normal): back-facing triangles never pass, and a front-facing one needs the margin
-        // 17.5 u rho_t / g_t + c (g_t: its determinant bound), or the rigorous one when g_t <= 0
-        {
-          const bool fast_ok = cluster_may_pass(L, H, o, inv, KF) &&
-                               cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, KF);
-          bool ok = fast_ok, ok_q = fast_ok;
-          if (!fast_ok && K > KF) {
-            ref_susp++;
-            ref_items += inf.y;
-            double Kp = -1, Kq = -1;
-            for (int k = 0; k < inf.y; k++) {
-              const float4 a = cs.ce1[inf.x + k], b = cs.ce2[inf.x + k];
-              const double Nx = (double)a.y * b.z - (double)a.z * b.y, Ny = (double)a.z * b.x - (double)a.x * b.z,
-                           Nz = (double)a.x * b.y - (double)a.y * b.x;
-              const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
-              const double la = std::sqrt((double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z);
-              const double lb = std::sqrt((double)b.x * b.x + (double)b.y * b.y + (double)b.z * b.z);
-              double Kt;
-              if (Nl == 0) {
-                if (la * lb <= 0.3) continue;
-                Kt = cs.kc[c].z;
-              } else {
-                const double rho = std::max(1.0, la * lb / Nl), u = ULP_HALF;
-                const double beta = 5.8 * u * rho * (1 + 1e-3) + 40 * u;
-                const double ndt = (Nx * d.x + Ny * d.y + Nz * d.z) / Nl;
-                if (ndt > beta) continue;  // back-facing: fl(a) < 0
-                const double g = -ndt - beta;
-                Kt = g > 0 ? std::min((double)cs.kc[c].z, 17.5 * u * rho / g + cs.kc[c].w) : cs.kc[c].z;
-              }
-              Kp = std::max(Kp, Kt);
-              const double q = Kt <= KF ? KF : (Kt <= 1e-3 ? 1e-3 : (Kt <= 1e-2 ? 1e-2 : (double)cs.kc[c].z));
-              Kq = std::max(Kq, q);
-            }
-            if (Kp < 0) ref_back++;
-            ok = Kp >= 0 && cluster_may_pass(L, H, o, inv, (float)std::max(Kp, 1e-4)) &&
-                 cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, (float)std::max(Kp, 1e-4));
-            ok_q = Kq >= 0 && cluster_may_pass(L, H, o, inv, (float)Kq) &&
-                   cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, (float)Kq);
-          }
-          // the compacted design: a pair not culled at the cluster level gets a normal round; every triangle
-          // that is front-facing and whose own margin reaches the pair's box is tested in full
-          {
-            const bool cheap_cull = K < 0 || (!fast_ok && K <= KF) ||
-                                    !(cluster_may_pass(L, H, o, inv, cs.kc[c].z) &&
-                                      cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, cs.kc[c].z));
-            if (!cheap_cull) {
-              cmp_rounds++;
-              for (int k = 0; k < inf.y; k++) {
-                const float4 a = cs.ce1[inf.x + k], b = cs.ce2[inf.x + k];
-                const double Nx = (double)a.y * b.z - (double)a.z * b.y, Ny = (double)a.z * b.x - (double)a.x * b.z,
-                             Nz = (double)a.x * b.y - (double)a.y * b.x;
-                const double Nl = std::sqrt(Nx * Nx + Ny * Ny + Nz * Nz);
-                const double la = std::sqrt((double)a.x * a.x + (double)a.y * a.y + (double)a.z * a.z);
-                const double lb = std::sqrt((double)b.x * b.x + (double)b.y * b.y + (double)b.z * b.z);
-                double Kt;
-                if (Nl == 0) {
-                  if (la * lb <= 0.3) continue;
-                  Kt = cs.kc[c].z;
-                } else {
-                  const double rho = std::max(1.0, la * lb / Nl), u = ULP_HALF;
-                  const double beta = 5.8 * u * rho * (1 + 1e-3) + 40 * u;
-                  const double ndt = (Nx * d.x + Ny * d.y + Nz * d.z) / Nl;
-                  if (ndt > beta) continue;
-                  const double g = -ndt - beta;
-                  Kt = g > 0 ? std::min((double)cs.kc[c].z, 17.5 * u * rho / g + cs.kc[c].w) : cs.kc[c].z;
-                }
-                const float Kf = (float)std::max(Kt, (double)KF);
-                const bool need = cluster_may_pass(L, H, o, inv, Kf) &&
-                                  cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, Kf);
-                cmp_items += need;
-                float bx, by, bz;
-                const bool p1 = tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, o, d, bx, by, bz) >= 1;
-                viol_cmp += p1 && !need;
-              }
-            } else {
-              viol_cmp += pass;
-            }
-          }
-          // two tiers (experiment): pairs that also miss the boxes widened at KD use masks built for KD
-          if (!fast_ok) {
-            const bool nearp = cluster_may_pass(L, H, o, inv, KD) &&
-                               cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, KD);
-            const int bk = dir_bucket(d, mask_n);
-            const unsigned long long mk = nearp ? masks[(size_t)c * 6 * mask_n * mask_n + bk]
-                                                : masks2[(size_t)c * 6 * mask_n * mask_n + bk];
-            t2_near += nearp;
-            t2_items += __builtin_popcountll(mk);
-            for (int k = 0; k < inf.y; k++) {
-              float bx, by, bz;
-              const bool p1 = tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, o, d, bx, by, bz) >= 1;
-              viol_t2 += p1 && !((mk >> k) & 1ull);
-            }
-          }
-          // the product's exact cull: a fast-box hit is swept; a miss walks its danger mask and tests the
-          // triangles danger_needs_test keeps
-          if (!fast_ok) {
-            const int bk = dir_bucket(d, mask_n);
-            const unsigned long long mk = masks[(size_t)c * 6 * mask_n * mask_n + bk];
-            const float Dm = box_miss(L, H, o, inv);
-            msk_items += __builtin_popcountll(mk);
-            msk_pairs += mk != 0ull;
-            for (int k = 0; k < inf.y; k++) {
-              const bool need = ((mk >> k) & 1ull) && danger_needs_test(tn[64 * (size_t)c + k], d, Dm, cm.c);
-              msk_needed += need;
-              float bx, by, bz;
-              const bool p1 = tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, o, d, bx, by, bz) >= 1;
-              viol_msk += p1 && !need;
-            }
-          }
-          ref_sw += ok;
-          ref_tris += ok ? inf.y : 0;
-          refq_sw += ok_q;
-          viol_ref += pass && !ok_q;
-        }
         old_sw += ok_old;
-        new_sw += ok_new;
         old_tris += ok_old ? inf.y : 0;
-        new_tris += ok_new ? inf.y : 0;
-        graze_tris += (ok_new && K >= 0 && !(-ndv - cs.kc[c].x > 0.0f)) ? inf.y : 0;
-        viol_old += pass && !ok_old;
-        viol_new += pass && !ok_new;
+        viol_old += passes && !ok_old;
+        const float ndv = n.x * d.x + n.y * d.y + n.z * d.z;
+        const bool hit = cluster_may_pass(L, H, o, inv, KF) &&
+                         cluster_may_pass_obb_k(L, H, n, cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], o, inv, d, ndv, KF);
+        if (hit) {
+          msk_sw++;
+          continue;
+        }
+        msk_missed++;
+        bool loaded;
+        int items;
+        const unsigned long long nm = mt.needs_all(bound, c, L, H, o, inv, d, loaded, items);
+        msk_loads += loaded;
+        msk_items += items;
+        msk_needed += __builtin_popcountll(nm);
+        viol_msk += (passes & ~nm) != 0ull;
       }
     }
   }
   const double R = (double)std::max(1LL, nr);
   printf("{\"rays\": %lld, \"clusters\": %zu, \"mode\": %d, \"chord\": %g, \"big_leaves_per_ray\": %.4f, "
-         "\"pairs_per_ray\": %.4f, \"sweeps_old\": %.4f, \"sweeps_new\": %.4f, \"productive\": %.4f, "
-         "\"back_per_ray\": %.4f, \"front_per_ray\": %.4f, \"graze_per_ray\": %.4f, \"viol_old\": %lld, "
-         "\"viol_new\": %lld, \"nofast\": %lld, \"small_tris\": %.3f, \"old_tris\": %.3f, \"new_tris\": %.3f, "
-         "\"graze_tris\": %.3f, \"ref_susp\": %.4f, \"ref_items\": %.3f, \"ref_back\": %.4f, \"ref_sweeps\": %.4f, "
-         "\"ref_tris\": %.3f, \"refq_sweeps\": %.4f, \"viol_ref\": %lld, \"cmp_rounds\": %.4f, \"cmp_items\": %.3f, "
-         "\"viol_cmp\": %lld, \"mask_n\": %d, \"msk_items\": %.3f, \"msk_pairs\": %.4f, \"viol_msk\": %lld, "
-         "\"msk_needed\": %.4f, \"t2_near\": %.4f, \"t2_items\": %.3f, \"viol_t2\": %lld}\n",
-         nr, cs.info.size(), grp.mode, grp.chord, leaves / R, pairs / R, old_sw / R, new_sw / R, prod / R, back / R,
-         front / R, graze / R, viol_old, viol_new, nofast, small_tris / R, old_tris / R, new_tris / R, graze_tris / R,
-         ref_susp / R, ref_items / R, ref_back / R, ref_sw / R, ref_tris / R, refq_sw / R, viol_ref, cmp_rounds / R,
-         cmp_items / R, viol_cmp, mask_n, msk_items / R, msk_pairs / R, viol_msk, msk_needed / R, t2_near / R,
-         t2_items / R, viol_t2);
+         "\"pairs_per_ray\": %.4f, \"sweeps_old\": %.4f, \"sweeps_masked\": %.4f, \"productive\": %.4f, "
+         "\"viol_old\": %lld, \"nofast\": %lld, \"small_tris\": %.3f, \"old_tris\": %.3f, \"mask_n\": %d, "
+         "\"msk_missed\": %.4f, \"msk_loads\": %.4f, \"msk_items\": %.4f, \"msk_needed\": %.4f, \"viol_msk\": %lld}\n",
+         nr, cs.info.size(), grp.mode, grp.chord, leaves / R, pairs / R, old_sw / R, msk_sw / R, prod / R, viol_old,
+         nofast, small_tris / R, old_tris / R, mt.n, msk_missed / R, msk_loads / R, msk_items / R, msk_needed / R,
+         viol_msk);
   return 0;
 }
 
@@ -452,6 +393,32 @@ int main(int argc, char** argv) {
     tv[i] = make_float4(T.x1, T.y1, T.z1, ibits(T.mtlIdx));
     e1[i] = make_float4(T.x2 - T.x1, T.y2 - T.y1, T.z2 - T.z1, 0.0f);
     e2[i] = make_float4(T.x3 - T.x1, T.y3 - T.y1, T.z3 - T.z1, 0.0f);
+  }
+  if (strcmp(argv[2], "--masks") == 0) {
+    // cull_diff TREE --masks OUT.bin: the masks and bound codes kdpt_create builds on the device for this tree
+    // (the scene's masked-cull coefficient and resolution), from the host builder: int32 n, int32 num_clusters,
+    // float Kf, uint64 masks[6 n^2][num_clusters], uint8 codes[6 n^2][num_clusters]
+    ClusterSet cs;
+    build_cluster_set(nodes.data(), nn, tris.data(), tv, e1, e2, cs);
+    const CullMargin cm = cluster_margin(cs.cv0, cs.ce1, cs.ce2);
+    const int n = mask_res((int)cs.info.size()), ncl = (int)cs.info.size();
+    std::vector<unsigned long long> masks;
+    std::vector<unsigned char> codes;
+    build_dir_masks(cs, n, cm.K, masks, codes);
+    FILE* g = fopen(argv[3], "wb");
+    if (!g) return 3;
+    const bool ok = fwrite(&n, 4, 1, g) == 1 && fwrite(&ncl, 4, 1, g) == 1 && fwrite(&cm.K, 4, 1, g) == 1 &&
+                    fwrite(masks.data(), 8, masks.size(), g) == masks.size() &&
+                    fwrite(codes.data(), 1, codes.size(), g) == codes.size();
+    fclose(g);
+    long long nz = 0, coded = 0;
+    for (size_t k = 0; k < masks.size(); k++) {
+      nz += masks[k] != 0ull;
+      coded += codes[k] != 0;
+    }
+    printf("{\"n\": %d, \"clusters\": %d, \"kf\": %.9g, \"exact\": %d, \"nonzero\": %lld, \"coded\": %lld, \"cells\": %zu}\n",
+           n, ncl, (double)cm.K, (int)cm.exact, nz, coded, masks.size());
+    return ok ? 0 : 3;
   }
   if (strcmp(argv[2], "--sim") == 0) {
     ClusterGrouping grp;
@@ -489,12 +456,9 @@ int main(int argc, char** argv) {
   const V3 sext = shi - slo;
   const double scale = std::max(sext.x, std::max(sext.y, sext.z));
 
-  const int mask_n = mask_res((int)cs.info.size());
   const float KF = mask_kf();
-  std::vector<unsigned long long> masks;
-  build_dir_masks(cs, mask_n, KF, masks);
-  std::vector<float4> tn;
-  build_entry_normals(cs, tn);
+  MaskTables mt;
+  mt.build(cs, mask_res((int)cs.info.size()), KF, cm.c);
   Counts tot[NGEN];
   const int nthreads = 1;
 #pragma omp parallel
@@ -648,15 +612,15 @@ int main(int argc, char** argv) {
                          cluster_may_pass_obb_k(L, H, cs.nrm[c], cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], of, inv, df, ndv,
                                                 KF);
         if (!hit) {
-          const unsigned long long mk = masks[(size_t)c * 6 * mask_n * mask_n + dir_bucket(df, mask_n)];
-          const float Dm = box_miss(L, H, of, inv);
-          C.mask_items += __builtin_popcountll(mk);
+          bool loaded;
+          int items;
+          const unsigned long long nm = mt.needs_all(true, c, L, H, of, inv, df, loaded, items);
+          C.mask_items += items;
+          C.mask_needed += __builtin_popcountll(nm);
           for (int k = 0; k < inf.y; k++) {
-            const bool need = ((mk >> k) & 1ull) && danger_needs_test(tn[64 * (size_t)c + k], df, Dm, cm.c);
-            C.mask_needed += need;
             float bx, by, bz;
             if (tri_test_v(TriData{cs.cv0[inf.x + k], cs.ce1[inf.x + k], cs.ce2[inf.x + k]}, of, df, bx, by, bz) >= 1 &&
-                !need)
+                !((nm >> k) & 1ull))
               C.viol_mask++;
           }
         }

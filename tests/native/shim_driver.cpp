@@ -2,7 +2,11 @@
 // pathtrace.cu (pathtraceInit, pathtrace per iteration with the flags of src/main.cpp:1152-1166,
 // pathtraceFree), with a Scene filled from the product's own scene builder.  Writes scene->state.image
 // after the last iteration (3*W*H floats).
-//   shim_driver SCENE.txt OBJ|- W H ITERS OUT.f32 [softness dof sss shortstack compaction enablekd]
+//   shim_driver SCENE.txt OBJ|- W H ITERS OUT.f32 [softness dof sss shortstack compaction enablekd [reinits]]
+// reinits: that many more times, pathtraceFree + pathtraceInit and the iterations again from 1 (what runCuda does
+// after a camera move, src/main.cpp:1134-1137); the image written is the last run's, and the JSON line carries
+// every pathtraceInit's wall time.
+#include <chrono>
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
@@ -48,15 +52,24 @@ int main(int argc, char** argv) {
   s.polyidxcount = v.polyidxcount;
   s.obj_bboxes = const_cast<float*>(v.obj_bboxes);
   std::vector<uchar4> pbo((size_t)W * H);
-  pathtraceInit(&s, enablekd);
-  for (int it = 1; it <= iters; it++)
-    pathtrace(pbo.data(), 0, it, 6.0f, dof, false, true, softness, sss, false, compaction, enablekd, false, false,
-              shortstack);
+  const int reinits = argc > 13 ? atoi(argv[13]) : 0;
+  std::vector<double> init_ms;
+  for (int run = 0; run <= reinits; run++) {
+    if (run > 0) pathtraceFree(&s, enablekd);
+    const auto t0 = std::chrono::steady_clock::now();
+    pathtraceInit(&s, enablekd);
+    init_ms.push_back(std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count());
+    for (int it = 1; it <= iters; it++)
+      pathtrace(pbo.data(), 0, it, 6.0f, dof, false, true, softness, sss, false, compaction, enablekd, false, false,
+                shortstack);
+  }
   FILE* f = fopen(argv[6], "wb");
   fwrite(s.state.image.data(), sizeof(float), 3 * (size_t)W * H, f);
   fclose(f);
   pathtraceFree(&s, enablekd);
   kdpt_scene_free(sd);
-  printf("{\"W\": %d, \"H\": %d, \"iterations\": %d}\n", W, H, iters);
+  printf("{\"W\": %d, \"H\": %d, \"iterations\": %d, \"init_ms\": [", W, H, iters);
+  for (size_t k = 0; k < init_ms.size(); k++) printf("%s%.3f", k ? ", " : "", init_ms[k]);
+  printf("]}\n");
   return 0;
 }

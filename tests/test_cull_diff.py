@@ -95,7 +95,8 @@ def test_c5_margin_is_rigorous_and_never_drops_a_pass(cull_diff, trees):
 
 @pytest.mark.parametrize("mesh", ["dragon_5", "icosphere_7"])
 def test_rigorous_margin_never_drops_a_pass(cull_diff, trees, mesh):
-    """Meshes whose rigorous margin is above the cap (so the kernels use the fast 1e-4): with the rigorous
+    """Meshes whose rigorous margin is above the cap (so the kernels use the masked cull's box coefficient 1e-3):
+    with the rigorous
     coefficient the cull drops no u/v pass either (10^7 adversarial lines for dragon_5's large triangles)."""
     probe = run(cull_diff, trees(mesh), 7, 1)
     n = 10_000_000 if mesh == "dragon_5" else 3_000_000
@@ -105,11 +106,12 @@ def test_rigorous_margin_never_drops_a_pass(cull_diff, trees, mesh):
 
 
 def test_fast_margin_is_not_rigorous_for_large_triangles(cull_diff, trees):
-    """dragon_5 with the fast margin alone (1e-4; the route of the "cull_exact" = 0 knob): the derived error
-    bound still holds for every pass, and the rounding-targeted generator does construct lines the fast box
-    cull drops while a triangle passes glm's u/v tests -- lines lying in a triangle's plane (to within rounding),
-    within ~1e-5 rad of parallel to it, passing beside the cluster's box.  The same lines keep every such
-    triangle in the direction mask the default (masked) cull selects: zero mask violations."""
+    """dragon_5 with the box coefficient alone (cm.K = CULL_MARGIN_MASKED = 1e-3, no masks: the route of the
+    "cull_exact" = 0 knob): the derived error bound still holds for every pass, and the rounding-targeted generator
+    does construct lines the box cull drops while a triangle passes glm's u/v tests -- lines lying in a triangle's
+    plane (to within rounding), within ~1e-5 rad of parallel to it, passing beside the cluster's box.  The same
+    lines keep every such triangle among those the default (masked) cull tests: zero mask violations, under each of
+    the three reciprocal perturbations (kd_rcp's 1-ulp error on the device)."""
     r = run(cull_diff, trees("dragon_5"), 2_000_000, 47)
     assert r["exact"] == 0 and r["margin"] < r["rigorous"], r
     assert 0 < r["bound"] <= 1.0, r
@@ -122,27 +124,35 @@ def test_fast_margin_is_not_rigorous_for_large_triangles(cull_diff, trees):
         assert r["gens"][g]["viol_box"] + r["gens"][g]["viol_slab"] + r["gens"][g]["viol_super"] == 0, (g, r)
 
 
-@pytest.mark.parametrize("mesh,n", [("dragon_5", 32), ("dragon_5", 16), ("dragon_5", 4), ("dragon_3", 32),
-                                    ("icosphere_7", 8)])
+@pytest.mark.parametrize("mesh,n", [("dragon_5", 128), ("dragon_5", 32), ("dragon_5", 16), ("dragon_5", 4),
+                                    ("dragon_3", 32), ("icosphere_7", 8)])
 def test_direction_masks_never_drop_a_pass(cull_diff, trees, mesh, n):
     """The masked one-level cull (kdpt_clusters.h build_dir_masks; the default for every scene whose rigorous
-    margin is above the cap): for every adversarial line, every triangle that passes glm's u/v tests is in the
-    mask the kernel selects (front mask when the line hits the cluster's fast-margin box and oriented box,
-    danger mask otherwise), at several cube-map resolutions."""
+    margin is above the cap): for every adversarial line that misses a cluster's box or oriented box at the box
+    coefficient, every triangle that passes glm's u/v tests is among those the kernel still tests -- the cell's
+    bound code lets the line through (kdpt_device.h mask_bound), the danger mask holds the triangle and
+    danger_needs_test keeps it -- with the reciprocal of dir_bucket / box_miss moved by -1, 0 and +1 ulp, at
+    several cube-map resolutions including the shipped 128 cells."""
     r = run(cull_diff, trees(mesh), 3_000_000 if mesh == "dragon_5" else 1_000_000, 53 + n, env={"MASK_N": str(n)})
     assert r["viol_mask"] == 0, r
     assert r["pass"] > 50_000, r
     assert r["gens"]["round"]["pass"] > 0, r
 
 
-def test_real_rays_through_the_traversal_keep_every_pass(cull_diff, trees, rays_c3):
+@pytest.mark.parametrize("n", [128, 32])
+def test_real_rays_through_the_traversal_keep_every_pass(cull_diff, trees, rays_c3, n):
     """Rays of a real C3 render walked through the traversal (tests/native/cull_diff.cpp --sim): at every big
-    leaf they visit, no cluster triangle that passes glm's u/v tests is left out of the selected mask, and the
-    masked cull tests about as many triangles per ray as the fast one swept (no perf cliff: at most 1.5x)."""
-    r = run(cull_diff, trees("dragon_5"), "--sim", rays_c3, 0, env={"MASK_N": "32"})
+    leaf they visit, every cluster triangle that passes glm's u/v tests is swept or tested by the masked cull
+    (under the three reciprocal perturbations), at the shipped 128 cells and at 32; the masked cull tests about
+    as many triangles per ray as the fast one swept (no perf cliff: at most 1.5x), and the bound codes spare most
+    missed pairs their mask load."""
+    r = run(cull_diff, trees("dragon_5"), "--sim", rays_c3, 0, env={"MASK_N": str(n)})
+    assert r["mask_n"] == n, r
     assert r["viol_msk"] == 0 and r["viol_old"] == 0, r
     assert r["big_leaves_per_ray"] > 0.1, r
     assert r["msk_items"] <= 1.5 * r["sweeps_old"] * 64, r
+    if n == 128:
+        assert r["msk_loads"] < 0.4 * r["msk_missed"], r
 
 
 def test_slivers_force_the_direction_free_margin(cull_diff, tmp_path):
