@@ -222,10 +222,16 @@ def main():
     sd = SceneData.from_description(desc)
     W, H = sd.resolution
     opt = default_options(testing_mode=1, short_stack=0 if args.bare else 1, bounce_cap=args.bounce_cap)
+    from kdtreepathtraceroptimization_amd.runtime import set_process_tuning
+    for kv in args.tune:  # "process.NAME": a knob contexts start with (kdpt_set_tuning(NULL, ...))
+        name, val = kv.split("=", 1)
+        if name.startswith("process."):
+            set_process_tuning(name[len("process."):], float(val))
     pt = PathTracer(sd, opt, device=local)
     for kv in args.tune:
         name, val = kv.split("=", 1)
-        pt.set_tuning(name, float(val))
+        if not name.startswith("process."):
+            pt.set_tuning(name, float(val))
     # the framebuffer reduce: RCCL inside the library (kdpt_comm_init: rank 0's unique id handed out through
     # the process group), or -- gloo rehearsals, ranks sharing a GPU -- each rank's frame shares handed out
     # and reduced here over gloo

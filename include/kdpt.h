@@ -247,11 +247,12 @@ int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
  * "cull_exact" (1; 0 = for meshes of large triangles the margin-only cull instead of the masked exact one, not
  * exact), "cull_mask_n" (the direction masks' cube-map cells per face edge, 1 .. 128; default: the finest of
  * 128 / 64 / 32 ... within 160 MB), "cull_fast_k" (the masked cull's box coefficient, default 1e-3; the masks
- * are rebuilt for it), "cull_bound" (1; 0 = the masked cull reads every missed pair's danger mask instead of first
- * testing the line against its cell's bound, exact either way), "reduce_spin_us" (0; > 0: a device spin of that many
+ * are rebuilt for it), "reduce_spin_us" (0; > 0: a device spin of that many
  * microseconds on the reduce stream before every frame's reduce, emulating an ncclReduce that waits for a slower
  * peer -- a diagnostic of the frame pipeline; ctx = NULL sets it for contexts created later, e.g. the ones
- * kdpt_render_sharded creates), "sync_debug" (0).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots
+ * kdpt_render_sharded creates), "sync_debug" (0).  ctx = NULL only: "cluster_chord" (-1 = the default grouping;
+ * > 0: contexts created later group every big leaf's triangles into normal cones of that chord before the Morton
+ * runs -- an A/B of the cluster layout; the results are the same bits).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots
  * (they are remade). */
 int kdpt_set_tuning(kdpt_ctx *ctx, const char *name, double value);
 /* The intersect kernel's configuration: tree source (0 HBM 64-byte records, 1 HBM 32-byte, 2 LDS 32-byte,
@@ -270,11 +271,11 @@ int kdpt_trace_config(kdpt_ctx *ctx, int *tree_mode, int *block, int *grid, long
  * culled at the box coefficient (1e-3) without masks: the cull is then conservative except for rays nearly
  * coplanar with a triangle. */
 int kdpt_cull_margin(kdpt_ctx *ctx, float *margin, double *rigorous, int *exact);
-/* The masked cull's tables as the device built them (bucket-major: cell b * num_clusters + c, 6 mask_n^2 buckets):
- * danger masks and bound codes.  *mask_n = 0 when the scene has none (its cull is exact without them).  masks /
- * codes may be NULL (sizes only); otherwise 6 mask_n^2 num_clusters entries each.  For parity tests against the
- * host builder (kdpt_clusters.h build_dir_masks). */
-int kdpt_cull_masks(kdpt_ctx *ctx, int *mask_n, int *num_clusters, unsigned long long *masks, uint8_t *codes);
+/* The masked cull's danger masks as the device built them (bucket-major: cell b * num_clusters + c, 6 mask_n^2
+ * buckets).  *mask_n = 0 when the scene has none (its cull is exact without them).  masks may be NULL (sizes
+ * only); otherwise 6 mask_n^2 num_clusters entries.  For parity tests against the host builder
+ * (kdpt_clusters.h build_dir_masks). */
+int kdpt_cull_masks(kdpt_ctx *ctx, int *mask_n, int *num_clusters, unsigned long long *masks);
 
 /* ---- Multi-GPU: samples per pixel sharded across GPUs ----
  * Frame f covers global iterations f*spp + 1 .. (f+1)*spp (the RNG seeds, iteration 2's sort and cacherays

@@ -445,7 +445,7 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
 // (dir_bucket: a cube map of n x n cells per face, nb = 6 n^2 buckets), masks[b ncl + c] = the danger mask over
 // the cluster's 64 entries: the triangles that, for SOME direction of the bucket, are front-facing and need a
 // margin above Kf -- the coefficient of the fast box test a pair's line missed (and whose rigorous coefficient
-// exceeds Kf; codes[b ncl + c] bounds those coefficients, mask_bound_code).  A triangle t needs the margin
+// exceeds Kf).  A triangle t needs the margin
 // K_t(d) = 17.5 u rho_t / g_t + c (g_t = -N_t/|N_t| . d - beta_t; danger_needs_test), above Kf only when
 // g_t < 17.5 u rho_t / (Kf - c).  Every other triangle of such a cluster is back-facing for the whole bucket
 // (its float determinant negative) or lies farther from the line than its own error bound: it cannot pass glm's
@@ -529,28 +529,21 @@ inline void mask_buckets(int n, std::vector<double>& bd) {
   }
 }
 
-// The masks and their bound codes on the host, bucket-major (masks[b ncl + c], codes likewise: DevScene::cl_mask,
-// cl_mq).  Test infrastructure: the product builds the same cells on the device (kdpt_runtime.hip k_build_masks,
-// the same dir_mask_cell over the same entries and buckets; tests/test_gpu_parity.py compares the two).
-inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<unsigned long long>& masks,
-                            std::vector<unsigned char>& codes) {
+// The masks on the host, bucket-major (masks[b ncl + c]: DevScene::cl_mask).  Test infrastructure: the product
+// builds the same cells on the device (kdpt_runtime.hip k_build_masks, the same dir_mask_cell over the same
+// entries and buckets; tests/test_gpu_masks.py compares the two).
+inline void build_dir_masks(const ClusterSet& cs, int n, float Kf, std::vector<unsigned long long>& masks) {
   const int ncl = (int)cs.info.size(), nb = 6 * n * n;
   MaskEntries me;
   mask_entries(cs, Kf, me);
   std::vector<double> bd;
   mask_buckets(n, bd);
   masks.assign((size_t)nb * ncl, 0ull);
-  codes.assign((size_t)nb * ncl, 0);
   auto work = [&](int c) {  // cluster by cluster: its 64 entries stay in cache over the buckets
     const size_t q0 = 64 * (size_t)c;
-    for (int b = 0; b < nb; b++) {
-      unsigned long long md;
-      uint32_t code;
-      dir_mask_cell(&me.nx[q0], &me.ny[q0], &me.nz[q0], &me.beta[q0], &me.dthr[q0], &me.krig[q0], &bd[4 * (size_t)b],
-                    Kf, md, code);
-      masks[(size_t)b * ncl + c] = md;
-      codes[(size_t)b * ncl + c] = (unsigned char)code;
-    }
+    for (int b = 0; b < nb; b++)
+      masks[(size_t)b * ncl + c] = dir_mask_cell(&me.nx[q0], &me.ny[q0], &me.nz[q0], &me.beta[q0], &me.dthr[q0],
+                                                 &me.krig[q0], &bd[4 * (size_t)b], Kf);
   };
   const int nth = (int)std::max(1u, std::min(16u, std::thread::hardware_concurrency()));
   std::vector<std::thread> th;

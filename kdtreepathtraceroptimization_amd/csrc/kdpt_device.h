@@ -153,10 +153,6 @@ struct DevScene {
   // (tuning "cull_exact" = 0) or no one-level cull at all
   const unsigned long long* cl_mask;  // [6 mask_n^2][num_clusters] danger masks
   int mask_n;                          // cube-map cells per face edge (dir_bucket)
-  // ... and per (bucket, cluster), in the same order, the code of a bound on the rigorous coefficients of the
-  // mask's triangles (mask_bound_code: 0 = the mask is never needed); null: every missed pair reads its mask
-  // (tuning "cull_bound" = 0)
-  const unsigned char* cl_mq;
   // per cluster entry: the triangle's unit normal (float) and 17.5 u rho (the exact cull's per-triangle
   // bound); w = -1: never passes (padding, small degenerate), w = +inf: may pass for any direction
   const float4* cl_tn;
@@ -669,45 +665,22 @@ KDPT_HD bool danger_needs_test(float4 tn, f3 d, float D, float c) {
   return !(g > 0.0f) || tn.w * 1.00001f >= (D - c) * g;
 }
 
-// The bound codes of the masked cull (DevScene::cl_mq).  Every triangle t has a direction-free rigorous
-// coefficient K_t = 8.75 |e1||e2| + c ("Cluster cull": a line glm's float u/v tests accept for t
-// passes within K_t W of any region holding t), so a (line, cluster) pair whose line misses the cluster's box at
-// the largest K_t of the mask's triangles needs none of them.  Code q in 1 .. 254 stands for the exact float
-// mask_bound(q) = (17 + q % 16) 2^(q / 16 - 14) (1.1e-3 .. 64, steps of at most 1/17); 0: the mask is empty (or
-// each of its K_t is at most the box coefficient Kf, which the pair already missed); 255: no bound.  The same
-// float on the host and on gfx950 (ldexp is exact), so the encoder's comparisons hold on both.
-KDPT_HD float mask_bound(uint32_t q) { return ldexpf((float)(17u + (q & 15u)), (int)(q >> 4) - 14); }
-KDPT_HD uint32_t mask_bound_code(float Kb, float Kf) {
-  if (Kb <= Kf) return 0u;
-  uint32_t lo = 1u, hi = 255u;  // the smallest q in 1 .. 254 with mask_bound(q) >= Kb; 255 if none (or NaN)
-  while (lo < hi) {
-    const uint32_t mid = (lo + hi) >> 1;
-    if (mask_bound(mid) >= Kb) hi = mid;
-    else lo = mid + 1u;
-  }
-  return lo;
-}
-
 // One (bucket, cluster) cell of the masked cull (kdpt_clusters.h build_dir_masks on the host and k_build_masks on
 // the device run this same code, -ffp-contract=off, so both give the same bits).  Per entry k of the cluster: its
 // unit normal n_k, beta_k and dthr_k (kdpt_clusters.h mask_entries) and its rigorous coefficient krig_k; the
 // bucket: its centre direction D[0..2] and radius D[3].  Entry k is in the danger mask when some direction of the
-// bucket makes it front-facing (n_k . d <= beta_k) and needing more than Kf (n_k . d >= dthr_k), and K_t > Kf
-// (otherwise the missed box test at Kf already covers it); the code bounds the krig of the mask's entries.
-KDPT_HD void dir_mask_cell(const double* nx, const double* ny, const double* nz, const double* beta,
-                           const double* dthr, const float* krig, const double* D, float Kf,
-                           unsigned long long& mask, uint32_t& code) {
+// bucket makes it front-facing (n_k . d <= beta_k) and needing more than Kf (n_k . d >= dthr_k), and its own
+// direction-free rigorous coefficient K_t = 8.75 |e1||e2| + c exceeds Kf (a line glm's float u/v tests accept for
+// t passes within K_t W of any region holding t -- DESIGN.md 4, "Cluster cull" -- so a pair that missed the box
+// or the oriented box at Kf >= K_t cannot need t).
+KDPT_HD unsigned long long dir_mask_cell(const double* nx, const double* ny, const double* nz, const double* beta,
+                                         const double* dthr, const float* krig, const double* D, float Kf) {
   unsigned long long md = 0ull;
-  float kb = 0.0f;
   for (int k = 0; k < 64; k++) {
     const double x = nx[k] * D[0] + ny[k] * D[1] + nz[k] * D[2];
-    if (x - D[3] <= beta[k] && x + D[3] >= dthr[k] && krig[k] > Kf) {
-      md |= 1ull << k;
-      kb = krig[k] > kb ? krig[k] : kb;
-    }
+    if (x - D[3] <= beta[k] && x + D[3] >= dthr[k] && krig[k] > Kf) md |= 1ull << k;
   }
-  mask = md;
-  code = md ? mask_bound_code(kb, Kf) : 0u;
+  return md;
 }
 
 #if defined(__HIPCC__) || defined(__HIP__)
@@ -1301,7 +1274,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     // Sweeps of the (ray, cluster) pairs `pass` marks: cluster c with the ray of lane own, each surviving
     // cluster by the whole wave, the next survivor's triangles fetched while this one is tested; the results
     // are folded into the owner lane's k_* (order-free).  Wave-uniform call.
-    auto sweep64 = [&](bool pass, int c, int own) {
+    auto sweep64 = [&](bool pass, int c, int own, auto&& mid) {
       unsigned long long sm = __ballot(pass);
       int s = -1;
       TriData T{};
@@ -1311,6 +1284,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         const int ct = __builtin_amdgcn_readlane(c, s) * 64 + lane;
         T = TriData{S.c_v0[ct], S.c_e1[ct], S.c_e2[ct]};
       }
+      mid();  // (after the first survivor's loads: vector loads complete in issue order)
       while (s >= 0) {
         int sn = -1;
         TriData Tn{};
@@ -1453,7 +1427,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     };
     auto sweep = [&](bool pass, int c, int own) {
       if constexpr (CLUSTER == 32) sweep32(pass, c, own);
-      else sweep64(pass, c, own);
+      else sweep64(pass, c, own, [] {});
     };
     const int ncl = big ? (lsize + CLUSTER - 1) / CLUSTER : 0;
     if constexpr (ClusterSrc::kSuper) {
@@ -1566,9 +1540,8 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       // With direction masks (S.cl_mask: the exact cull, DESIGN.md 4 "Cluster cull") a miss may still hide a
       // u/v pass of a triangle nearly parallel to the line: the cluster's danger mask for the ray's direction
       // bucket (kdpt_clusters.h build_dir_masks) lists every triangle that can need more than cl_margin for
-      // some direction of the bucket.  The cell's bound code (S.cl_mq, one byte, requested with the box test)
-      // says whether the mask can matter for this line at all; only then is the mask requested, before the
-      // pass's sweeps, and read after them (its latency hidden behind them); the lane then walks its bits, deciding each
+      // some direction of the bucket.  The mask is requested with the box test and read after the pass's
+      // sweeps (its latency hidden behind them); the missed pair's lane then walks its bits, deciding each
       // triangle from its unit normal and the line's box_miss distance (danger_needs_test), and the rare one
       // that needs it gets glm's u/v tests.  A pass sweeps the whole cluster late, as the uncull'd walk would
       // have: the sweep's results fold by max / min / sum, so a late sweep is the same as an early one.
@@ -1589,18 +1562,24 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         const int c = W->tbase[own] + B + lane;
         bool hit = B + lane < P;  // (no cull: every pair swept)
         unsigned long long m = 0ull;  // a missed pair's danger mask (exact cull)
+#ifdef KDPT_MASK_MID
+        uint32_t mmi = 0u;  // (A/B) the missed pair's cell + 1: its mask is read once the sweep's first loads are out
+#endif
         if (fastAABB) {
           const float4 od = W->od[own];  // the pair's ray from the wave's LDS copy (wave_ray_start)
           const float2 d2 = W->dd[own];
           const f3 oo = mk3(od.x, od.y, od.z), dd = mk3(od.w, d2.x, d2.y);
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
           float4 clo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), chi = clo;
-          uint32_t mi = 0u, q = 0u;  // the pair's (bucket, cluster) cell and its bound code (exact cull)
+          unsigned long long dm = 0ull;
+          uint32_t mi = 0u;  // the pair's (bucket, cluster) cell (exact cull)
           const bool valid = hit;
           if (valid) {
             if (exact) {
               mi = (uint32_t)dir_bucket(dd, S.mask_n) * (uint32_t)S.num_clusters + (uint32_t)c;
-              q = S.cl_mq ? (uint32_t)S.cl_mq[mi] : 255u;
+#ifndef KDPT_MASK_MID
+              dm = S.cl_mask[mi];
+#endif
             }
             clo = clusters.lo_of(c);
             chi = clusters.hi_of(c);
@@ -1614,15 +1593,20 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
                                            cn.x * dd.x + cn.y * dd.y + cn.z * dd.z, S.cl_margin);
             }
           }
-          // a missed pair reads its danger mask only when its line also meets the cluster's box widened by
-          // the mask's bound (the mask's triangles' largest rigorous coefficient, mask_bound): most cells are
-          // empty or far, and skip the 8-byte load from the large table
-          if (exact && valid && !hit && q != 0u &&
-              (q == 255u || cluster_may_pass(clo, chi, oo, ii, mask_bound(q))))
-            m = S.cl_mask[mi];
+#ifdef KDPT_MASK_MID
+          if (exact && valid && !hit) mmi = mi + 1u;
+#else
+          if (exact && valid && !hit) m = dm;
+#endif
         }
         if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
+#ifdef KDPT_MASK_MID
+        sweep64(hit, c, own, [&] {
+          if (mmi) m = S.cl_mask[mmi - 1u];
+        });
+#else
         sweep(hit, c, own);
+#endif
         if (COUNT) prof_lap(WP, PROF_BIG_CYC);
         if (!exact || !__any(m != 0ull)) continue;
         bool late = false;  // a danger triangle passed glm's u/v tests: sweep the cluster now

@@ -47,6 +47,8 @@ constexpr int MAX_KEYS = 64;
 
 thread_local std::string g_last_error;
 double g_reduce_spin_us = 0;  // kdpt_set_tuning(NULL, "reduce_spin_us", v): the default of new contexts
+double g_cluster_chord = -1;   // kdpt_set_tuning(NULL, "cluster_chord", v): big-leaf grouping of new contexts
+bool g_cu_mask_streams = false;  // kdpt_set_tuning(NULL, "cu_mask_streams", 1): ... and their stream kind
 
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -1697,12 +1699,11 @@ struct kdpt_ctx {
   // the exact one-level cull's direction masks (kdpt_clusters.h build_dir_masks), built when the scene's rigorous
   // margin is above the cap; S.cl_mask points at them unless a knob chose another cull
   unsigned long long* mask_dev = nullptr;
-  unsigned char* mq_dev = nullptr;  // their bound codes (DevScene::cl_mq)
   float4* tn_dev = nullptr;  // the clusters' per-entry normal records (DevScene::cl_tn)
   int mask_n = 0;
   bool cull_exact = true;   // "cull_exact" knob: 0 = the fast-margin cull (not exact for such scenes)
-  bool cull_bound = true;   // "cull_bound" knob: 0 = every missed pair reads its mask (no bound codes)
   double create_ms = 0, mask_build_ms = 0;  // kdpt_create's host wall time, and the masks' (kdpt_stats)
+  bool cu_mask_streams = false;  // batch and reduce streams created with an all-CU mask (create_stream)
   bool cull_scene = true;   // false after "cluster_cull" = 0 or a fixed "cull_margin"
   std::unique_ptr<ClusterSet> mask_cs;  // the clusters the masks were built from ("cull_mask_n" rebuilds)
   int tree_format = 0;             // "tree_format" knob: 16 / 32 = LDS node records of that size only
@@ -1735,16 +1736,17 @@ struct kdpt_ctx {
   bool sync_debug = false;  // "sync_debug" = 1: synchronise and log after every launch
   // Pipelined iterations (kdpt_trace_iterations): extra slots, each a context sharing this one's
   // scene upload but owning its per-iteration buffers, stream and partial image; the partial
-  // images are added into `image` in iteration order on `accum_stream`.
+  // images are added into `image` in iteration order, each batch's add on the batch's own stream after the
+  // previous batch's add (acc_ev / acc_last: the chain).
   kdpt_ctx* parent = nullptr;
   std::vector<kdpt_ctx*> slots;
   int slot_batch = 1;
   int next_group = 0;  // the slot group the next batch goes to
   bool profile_batches = false;
   bool profile_steps = false;  // "profile_batches" = 2
-  std::vector<hipEvent_t> slot_done, slot_free;
-  hipStream_t accum_stream = nullptr;
-  hipEvent_t accum_ev = nullptr;  // recorded on accum_stream; c->stream waits on it (join_accum)
+  std::vector<hipEvent_t> acc_ev;  // per slot group: its last batch's add into the target done
+  hipEvent_t acc_last = nullptr;   // the most recent add (one of acc_ev): the next add follows it
+  hipEvent_t img_last = nullptr;   // the most recent frame reduce + image add (one of frame_ev)
   // intersect-kernel timing (testing_mode) of every iteration, read back at synchronisation
   std::vector<std::vector<hipEvent_t>> pending_ev;  // per launched iteration: 2 events per bounce
   std::vector<hipEvent_t> free_ev;
@@ -1768,13 +1770,29 @@ struct kdpt_ctx {
   float* frame_buf[2] = {nullptr, nullptr};
   float* frame_sum = nullptr;
   hipEvent_t frame_ev[2] = {nullptr, nullptr};      // frame_buf[k] consumed by its reduce
-  hipEvent_t frame_acc_ev[2] = {nullptr, nullptr};  // frame_buf[k]'s accumulations done
   hipStream_t reduce_stream = nullptr;  // the frames' reduces and image adds, beside the accumulation stream
   double reduce_spin_us = 0;  // "reduce_spin_us" knob: a device spin before every frame's reduce (a slow peer)
   std::vector<void*> host_reg;  // pageable host `out` ranges pinned for kdpt_render_frames (released at synchronize)
 };
 
 namespace {
+
+// A stream for the batches and the frame reduces: non-blocking, or (knob "cu_mask_streams", A/B) one created with
+// a mask of every CU -- such a stream gets a hardware queue of its own instead of one of the GPU_MAX_HW_QUEUES
+// (4 by default) that HIP multiplexes the process's other streams onto.
+int create_stream(kdpt_ctx* c, hipStream_t* st) {
+  if (c->cu_mask_streams) {
+    hipDeviceProp_t prop;
+    HIP_TRY(hipGetDeviceProperties(&prop, c->device));
+    const int n = std::max(1, prop.multiProcessorCount);
+    std::vector<uint32_t> mask((n + 31) / 32, 0xffffffffu);
+    if (n % 32) mask.back() = (1u << (n % 32)) - 1u;
+    HIP_TRY(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
+    return KDPT_OK;
+  }
+  HIP_TRY(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
+  return KDPT_OK;
+}
 
 template <typename T>
 int dalloc(kdpt_ctx* c, T** p, size_t n) {
@@ -1800,14 +1818,14 @@ int launch_batch(kdpt_ctx* const* cs, const int* iters, int nb, hipStream_t st, 
                  std::vector<hipEvent_t>* bev);
 
 // Work queued on the context's own stream that reads or writes `image` must follow the pipelined
-// accumulation (kdpt_trace_iterations adds partial images on accum_stream without a host sync).
+// accumulation (kdpt_trace_iterations adds partial images on the batch streams without a host sync) and the
+// frames' image adds (kdpt_render_frames, on the reduce stream).
 int join_accum(kdpt_ctx* c) {
-  if (!c->accum_stream) return KDPT_OK;
-  if (!c->accum_ev) HIP_TRY(hipEventCreateWithFlags(&c->accum_ev, hipEventDisableTiming));
-  HIP_TRY(hipEventRecord(c->accum_ev, c->accum_stream));
-  HIP_TRY(hipStreamWaitEvent(c->stream, c->accum_ev, 0));
+  if (c->acc_last) HIP_TRY(hipStreamWaitEvent(c->stream, c->acc_last, 0));
+  if (c->img_last) HIP_TRY(hipStreamWaitEvent(c->stream, c->img_last, 0));
   return KDPT_OK;
 }
+
 
 // stats.segments / seg_per_bounce / bounces of the iteration whose counts are in h_counts
 int segments_from_counts(kdpt_ctx* c) {
@@ -1883,6 +1901,15 @@ void destroy_slots(kdpt_ctx* c) {
   for (size_t k = c->slots.size(); k-- > 0;) kdpt_destroy(c->slots[k]);
 }
 
+// Drop the pipeline slots (their streams drained by the caller) and the add chain's events.
+void drop_slots(kdpt_ctx* c) {
+  destroy_slots(c);
+  for (auto e : c->acc_ev) (void)hipEventDestroy(e);
+  c->slots.clear();
+  c->acc_ev.clear();
+  c->acc_last = nullptr;
+}
+
 // share: the stream of the slot's group leader (a group's batches all run on the leader's stream), or null
 // for a leader, which creates its own
 int make_slot(kdpt_ctx* p, kdpt_ctx** out, hipStream_t share = nullptr) {
@@ -1919,11 +1946,12 @@ int make_slot(kdpt_ctx* p, kdpt_ctx** out, hipStream_t share = nullptr) {
   c->num_shapes = p->num_shapes;
   c->chunk_lo = p->chunk_lo;
   c->chunk_hi = p->chunk_hi;
+  c->cu_mask_streams = p->cu_mask_streams;
   int rc;
   if (share) {
     c->stream = share;
     c->owns_stream = false;
-  } else if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess) {
+  } else if (create_stream(c, &c->stream) != KDPT_OK) {
     kdpt_destroy(c);
     return fail(KDPT_ERR_HIP, "hipStreamCreate failed");
   }
@@ -1984,17 +2012,15 @@ void fix_cull(kdpt_ctx* c, float K) {
 // margins in place, else the margin-only cull.
 void apply_cull_route(kdpt_ctx* c) {
   c->S.cl_mask = (c->mask_dev && c->cull_exact && c->cull_scene) ? c->mask_dev : nullptr;
-  c->S.cl_mq = (c->S.cl_mask && c->cull_bound) ? c->mq_dev : nullptr;
   c->S.mask_n = c->mask_n;
   c->S.cl_tn = c->tn_dev;
 }
 // The masked cull's cells on the device (kdpt_device.h dir_mask_cell, the code the host builder runs): one
 // workgroup per (cluster, 256 buckets), the cluster's 64 entries staged in LDS (every lane reads the same entry:
-// a broadcast), one mask and one bound code per lane, written bucket-major.
+// a broadcast), one mask per lane, written bucket-major.
 __global__ void __launch_bounds__(256) k_build_masks(const double* __restrict__ ent, const float* __restrict__ krig,
                                                      const double* __restrict__ bd, int ncl, int nb, float Kf,
-                                                     unsigned long long* __restrict__ masks,
-                                                     unsigned char* __restrict__ codes) {
+                                                     unsigned long long* __restrict__ masks) {
   __shared__ double se[5][64];
   __shared__ float sk[64];
   const int c = blockIdx.x;
@@ -2006,11 +2032,7 @@ __global__ void __launch_bounds__(256) k_build_masks(const double* __restrict__ 
   __syncthreads();
   const int b = blockIdx.y * 256 + threadIdx.x;
   if (b >= nb) return;
-  unsigned long long m;
-  uint32_t q;
-  dir_mask_cell(se[0], se[1], se[2], se[3], se[4], sk, bd + 4 * (size_t)b, Kf, m, q);
-  masks[(size_t)b * ncl + c] = m;
-  codes[(size_t)b * ncl + c] = (unsigned char)q;
+  masks[(size_t)b * ncl + c] = dir_mask_cell(se[0], se[1], se[2], se[3], se[4], sk, bd + 4 * (size_t)b, Kf);
 }
 
 // Release one of the context's device allocations before kdpt_destroy (a rebuilt table).
@@ -2021,8 +2043,7 @@ void dfree(kdpt_ctx* c, void* p) {
   (void)hipFree(p);
 }
 
-// The direction masks of the scene's clusters at resolution n (cube-map cells per face edge) and their bound
-// codes, built on the device (k_build_masks) from the per-entry records and the bucket directions the host
+// The direction masks of the scene's clusters at resolution n (cube-map cells per face edge), built on the device (k_build_masks) from the per-entry records and the bucket directions the host
 // computes (kdpt_clusters.h mask_entries / mask_buckets; tests/test_gpu_parity.py checks the cells against the
 // host builder).  A rebuild (knobs "cull_mask_n", "cull_fast_k") frees the previous tables.
 int build_masks(kdpt_ctx* c, int n) {
@@ -2044,17 +2065,12 @@ int build_masks(kdpt_ctx* c, int n) {
     ent[4 * ne + k] = me.dthr[k];
   }
   dfree(c, c->mask_dev);
-  dfree(c, c->mq_dev);
   c->mask_dev = nullptr;
-  c->mq_dev = nullptr;
   c->S.cl_mask = nullptr;
-  c->S.cl_mq = nullptr;
   unsigned long long* dm = nullptr;
-  unsigned char* dq = nullptr;
   int rc;
-  if ((rc = dalloc(c, &dm, (size_t)nb * ncl)) || (rc = dalloc(c, &dq, (size_t)nb * ncl))) return rc;
+  if ((rc = dalloc(c, &dm, (size_t)nb * ncl))) return rc;
   c->mask_dev = dm;
-  c->mq_dev = dq;
   double* d_ent = nullptr;
   float* d_krig = nullptr;
   double* d_bd = nullptr;
@@ -2077,7 +2093,7 @@ int build_masks(kdpt_ctx* c, int n) {
     return fail(KDPT_ERR_HIP, "mask build: device buffers");
   }
   hipLaunchKernelGGL(k_build_masks, dim3(ncl, (nb + 255) / 256), dim3(256), 0, c->stream, d_ent, d_krig, d_bd, ncl,
-                     nb, Kf, dm, dq);
+                     nb, Kf, dm);
   const hipError_t e1 = hipGetLastError(), e2 = hipStreamSynchronize(c->stream);
   release();
   if (e1 != hipSuccess || e2 != hipSuccess) return fail(KDPT_ERR_HIP, "k_build_masks failed");
@@ -2097,6 +2113,13 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
                    const std::vector<float4>& e2, std::vector<int2>& leaf_cl, std::vector<int2>& leaf_sp) {
   ClusterSet cs;
   build_cluster_set(sc->nodes, sc->num_nodes, sc->tris, tv, e1, e2, cs);
+  // (A/B: "cluster_chord" > 0 groups every big leaf's triangles by normal cones of that chord first)
+  if (g_cluster_chord > 0) {
+    ClusterGrouping g;
+    g.mode = 1;
+    g.chord = g_cluster_chord;
+    build_cluster_set(sc->nodes, sc->num_nodes, sc->tris, tv, e1, e2, cs, g);
+  }
   leaf_cl = cs.leaf_cl;
   leaf_sp = cs.leaf_sp;
   const std::vector<int4>& sp = cs.sup;
@@ -2681,6 +2704,7 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   HIP_TRY(hipDeviceSynchronize());
   if ((rc = kdpt_reset(c))) return bail(rc);
   c->reduce_spin_us = g_reduce_spin_us;
+  c->cu_mask_streams = g_cu_mask_streams;
   c->create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_create).count();
   *out = c;
   return KDPT_OK;
@@ -2723,6 +2747,15 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     g_reduce_spin_us = value;
     return KDPT_OK;
   }
+  if (!c && name && std::string(name) == "cu_mask_streams") {  // ... the kind of their batch / reduce streams
+    g_cu_mask_streams = value != 0.0;
+    return KDPT_OK;
+  }
+  if (!c && name && std::string(name) == "cluster_chord") {  // ... and their big-leaf cluster grouping
+    if (!(value >= -1.0 && value <= 4.0)) return fail(KDPT_ERR_ARG, "cluster_chord must be in [-1, 4]");
+    g_cluster_chord = value;
+    return KDPT_OK;
+  }
   if (!c || !name) return fail(KDPT_ERR_ARG, "null arg");
   if (c->parent) return fail(KDPT_ERR_ARG, "not a top-level context");
   HIP_TRY(hipSetDevice(c->device));
@@ -2731,12 +2764,7 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
   if (!c->slots.empty()) {
     int rc = kdpt_synchronize(c);
     if (rc) return rc;
-    destroy_slots(c);
-    for (auto e : c->slot_done) (void)hipEventDestroy(e);
-    for (auto e : c->slot_free) (void)hipEventDestroy(e);
-    c->slots.clear();
-    c->slot_done.clear();
-    c->slot_free.clear();
+    drop_slots(c);
   }
   const std::string k(name);
   const int v = (int)value;
@@ -2779,7 +2807,7 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     if (rc) return rc;
     if (c->grid_env) c->trace_grid = std::max(1, (int)(c->full_trace_grid * frac));
   } else if (k == "cluster_cull" || k == "cull_margin" || k == "cull_exact" || k == "cull_mask_n" ||
-             k == "cull_fast_k" || k == "cull_bound") {
+             k == "cull_fast_k") {
     if (k == "cluster_cull") {
       // 0: no cluster / chunk cull at all (every big-leaf cluster swept: exact by construction, whatever the
       // scene's margin); 1: the scene's margins (and masks)
@@ -2795,10 +2823,6 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
     } else if (k == "cull_exact") {
       // 0: the fast-margin one-level cull instead of the masked exact one (A/B; not exact for such scenes)
       c->cull_exact = v != 0;
-    } else if (k == "cull_bound") {
-      // 0: the masked cull reads every missed pair's mask instead of first checking its cell's bound code (A/B;
-      // exact either way)
-      c->cull_bound = v != 0;
     } else if (k == "cull_fast_k") {
       // the masked cull's box coefficient (default CULL_MARGIN_MASKED), its direction masks rebuilt for it: a
       // wider box sweeps more clusters, a narrower one leaves more danger triangles to decide
@@ -2837,7 +2861,7 @@ int kdpt_reset(kdpt_ctx* c) {
   if (!c) return fail(KDPT_ERR_ARG, "null ctx");
   HIP_TRY(hipSetDevice(c->device));
   for (auto sl : c->slots) HIP_TRY(hipStreamSynchronize(sl->stream));
-  if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
+  if (c->reduce_stream) HIP_TRY(hipStreamSynchronize(c->reduce_stream));
   drain_intersect_events(c);
   c->intersect_ms_total = 0;
   c->intersect_launches_total = 0;
@@ -2865,7 +2889,6 @@ int kdpt_synchronize(kdpt_ctx* c) {
     int rc = check_fault(sl);
     if (rc) return rc;
   }
-  if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
   if (c->reduce_stream) HIP_TRY(hipStreamSynchronize(c->reduce_stream));
   unregister_host(c);
   int rc = drain_intersect_events(c);
@@ -2905,28 +2928,26 @@ int kdpt_trace_iteration(kdpt_ctx* c, int frame, int iter) {
 
 // Iterations first_iter + k * stride (k < count) in batches of `batch`, `pipeline` batches in flight, their
 // partial images added into `target` (the context's image, or a frame buffer of kdpt_render_frames) in
-// iteration order on the accumulation stream.  Returns once everything is queued.
-int enqueue_iterations(kdpt_ctx* c, int first_iter, int count, int stride, int pipeline, int batch, float* target) {
+// iteration order.  Each batch's add runs on the batch's own stream, after the previous batch's add (the one
+// cross-stream wait of the pipeline, normally satisfied by the time it is reached): no stream ever waits for a
+// whole batch, so none holds an in-order hardware queue that batch streams share (HIP multiplexes a process's
+// streams onto GPU_MAX_HW_QUEUES queues, 4 by default).  zero_after: the target is first zeroed, after that
+// event (a frame buffer after its previous reduce).  Returns once everything is queued.
+int enqueue_iterations(kdpt_ctx* c, int first_iter, int count, int stride, int pipeline, int batch, float* target,
+                       hipEvent_t zero_after = nullptr) {
   const int depth = std::min(16, std::max(1, pipeline));
   const int B = std::min(MAXB, std::max(1, batch));
-  if (!c->accum_stream) HIP_TRY(hipStreamCreateWithFlags(&c->accum_stream, hipStreamNonBlocking));
-  // the accumulation follows everything already queued on the context's own stream (reset, ...)
+  // the first add follows everything already queued on the context's own stream (reset, ...)
   hipEvent_t entry;
-  HIP_TRY(hipEventCreate(&entry));
+  HIP_TRY(hipEventCreateWithFlags(&entry, hipEventDisableTiming));
   HIP_TRY(hipEventRecord(entry, c->stream));
-  HIP_TRY(hipStreamWaitEvent(c->accum_stream, entry, 0));
   // slots: `depth` groups of B iteration contexts; a group runs one batch at a time on its first
   // context's stream
   if ((int)c->slots.size() < depth * B || c->slot_batch != B) {
     if (!c->slots.empty()) {
       int rc = kdpt_synchronize(c);
       if (rc) return rc;
-      destroy_slots(c);
-      for (auto e : c->slot_done) (void)hipEventDestroy(e);
-      for (auto e : c->slot_free) (void)hipEventDestroy(e);
-      c->slots.clear();
-      c->slot_done.clear();
-      c->slot_free.clear();
+      drop_slots(c);
     }
     c->slot_batch = B;
     c->next_group = 0;
@@ -2941,15 +2962,12 @@ int enqueue_iterations(kdpt_ctx* c, int first_iter, int count, int stride, int p
       c->slots.push_back(sl);
     }
     for (int g = 0; g < depth; g++) {
-      hipEvent_t d, f;
+      hipEvent_t d;
       HIP_TRY(hipEventCreateWithFlags(&d, hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&f, hipEventDisableTiming));
-      HIP_TRY(hipEventRecord(f, c->accum_stream));
-      c->slot_done.push_back(d);
-      c->slot_free.push_back(f);
+      c->acc_ev.push_back(d);
     }
   }
-  const int ngroups = (int)c->slot_done.size();
+  const int ngroups = (int)c->acc_ev.size();
   // With several batches in flight each intersect launch gets a share of the chip (2/depth of the
   // persistent grid, all of it for depth <= 2, a quarter from depth 8 on): a launch's length is set by its
   // heaviest rays, so concurrent launches on disjoint CU subsets overlap those tails instead of queueing
@@ -2961,6 +2979,7 @@ int enqueue_iterations(kdpt_ctx* c, int first_iter, int count, int stride, int p
       c->slots.empty() ? 1.0f : (float)c->slots[0]->trace_grid / (float)std::max(1, c->full_trace_grid);
   // diagnostic ("profile_batches" knob): the counting intersect kernel (kdpt_wave_profile after sync)
   if (c->profile_batches) HIP_TRY(hipMemsetAsync(c->counters, 0, sizeof(Counters), c->stream));
+  bool first = true;
   for (int kb = 0; kb < count; kb += B) {
     const int nb = std::min(B, count - kb);
     // groups in turn, continuing across calls: kdpt_render_frames queues one call per frame, and a frame
@@ -2969,11 +2988,12 @@ int enqueue_iterations(kdpt_ctx* c, int first_iter, int count, int stride, int p
     c->next_group = (g + 1) % ngroups;
     kdpt_ctx* const* grp = &c->slots[(size_t)g * B];
     hipStream_t st = grp[0]->stream;
-    HIP_TRY(hipStreamWaitEvent(st, c->slot_free[g], 0));  // the group's last partial images were consumed
+    // (the group's previous batch's partial images were added on this stream, before this batch's camera rays
+    // clear them)
     int iters[MAXB];
     for (int b = 0; b < nb; b++) {
       iters[b] = first_iter + (kb + b) * stride;
-      grp[b]->zero_partial = true;  // k_gen_rays clears the partial image (after slot_free, on st)
+      grp[b]->zero_partial = true;  // k_gen_rays clears the partial image
     }
     std::vector<hipEvent_t>* bev = nullptr;
     if (c->opt.testing_mode) {
@@ -2989,16 +3009,26 @@ int enqueue_iterations(kdpt_ctx* c, int first_iter, int count, int stride, int p
     }
     int rc = launch_batch(grp, iters, nb, st, -1, c->profile_batches, bev);
     if (rc) return rc;
-    HIP_TRY(hipEventRecord(c->slot_done[g], st));
-    HIP_TRY(hipStreamWaitEvent(c->accum_stream, c->slot_done[g], 0));
+    // the add: after the previous add (the chain), and for the call's first batch after the context's stream,
+    // the frames' image adds (when the target is the image) and the target's zeroing
+    if (c->acc_last) HIP_TRY(hipStreamWaitEvent(st, c->acc_last, 0));
+    if (first) {
+      HIP_TRY(hipStreamWaitEvent(st, entry, 0));
+      if (c->img_last && target == c->image) HIP_TRY(hipStreamWaitEvent(st, c->img_last, 0));
+      if (zero_after) {
+        HIP_TRY(hipStreamWaitEvent(st, zero_after, 0));
+        HIP_TRY(hipMemsetAsync(target, 0, sizeof(float) * 3 * (size_t)c->npix, st));
+      }
+      first = false;
+    }
     const int n3 = 3 * c->npix;
     PartialImages parts{};
     parts.nb = nb;
     for (int b = 0; b < nb; b++) parts.p[b] = grp[b]->image;  // in iteration order
-    hipLaunchKernelGGL(k_accumulate_batch, dim3((n3 + 255) / 256), dim3(256), 0, c->accum_stream, target, parts,
-                       n3);
+    hipLaunchKernelGGL(k_accumulate_batch, dim3((n3 + 255) / 256), dim3(256), 0, st, target, parts, n3);
     HIP_TRY(hipGetLastError());
-    HIP_TRY(hipEventRecord(c->slot_free[g], c->accum_stream));
+    HIP_TRY(hipEventRecord(c->acc_ev[g], st));
+    c->acc_last = c->acc_ev[g];
   }
   HIP_TRY(hipEventDestroy(entry));
   c->stats.iterations += count;
@@ -3016,7 +3046,8 @@ int kdpt_trace_iterations(kdpt_ctx* c, int frame, int first_iter, int count, int
 int kdpt_read_image(kdpt_ctx* c, float* rgb) {
   if (!c || !rgb) return fail(KDPT_ERR_ARG, "null arg");
   HIP_TRY(hipSetDevice(c->device));
-  if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
+  int rc = join_accum(c);
+  if (rc) return rc;
   HIP_TRY(hipMemcpyAsync(rgb, c->image, sizeof(float) * 3 * (size_t)c->npix, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return KDPT_OK;
@@ -3072,7 +3103,7 @@ int kdpt_write_pbo(kdpt_ctx* c, int iter, uint8_t* rgba) {
 static int save_image_pass(kdpt_ctx* c, float samples, uint8_t* rgb, float* lin) {
   HIP_TRY(hipSetDevice(c->device));
   for (auto sl : c->slots) HIP_TRY(hipStreamSynchronize(sl->stream));
-  if (c->accum_stream) HIP_TRY(hipStreamSynchronize(c->accum_stream));
+  if (c->reduce_stream) HIP_TRY(hipStreamSynchronize(c->reduce_stream));
   const size_t n3 = 3 * (size_t)c->npix;
   uint8_t* d_rgb = nullptr;
   float* d_lin = nullptr;
@@ -3116,7 +3147,7 @@ int kdpt_save_hdr(kdpt_ctx* c, const char* path, float samples) {
   return rc ? fail(rc, std::string("cannot write ") + path) : KDPT_OK;
 }
 
-int kdpt_cull_masks(kdpt_ctx* c, int* mask_n, int* num_clusters, unsigned long long* masks, uint8_t* codes) {
+int kdpt_cull_masks(kdpt_ctx* c, int* mask_n, int* num_clusters, unsigned long long* masks) {
   if (!c || !mask_n || !num_clusters) return fail(KDPT_ERR_ARG, "null arg");
   HIP_TRY(hipSetDevice(c->device));
   *mask_n = c->mask_dev ? c->mask_n : 0;
@@ -3126,7 +3157,6 @@ int kdpt_cull_masks(kdpt_ctx* c, int* mask_n, int* num_clusters, unsigned long l
   HIP_TRY(hipStreamSynchronize(c->stream));
   if (masks)
     HIP_TRY(hipMemcpyAsync(masks, c->mask_dev, cells * sizeof(unsigned long long), hipMemcpyDeviceToHost, c->stream));
-  if (codes) HIP_TRY(hipMemcpyAsync(codes, c->mq_dev, cells, hipMemcpyDeviceToHost, c->stream));
   HIP_TRY(hipStreamSynchronize(c->stream));
   return KDPT_OK;
 }
@@ -3160,10 +3190,7 @@ int kdpt_destroy(kdpt_ctx* c) {
   if (!c) return KDPT_OK;
   (void)hipSetDevice(c->device);
   if (c->stream) (void)hipStreamSynchronize(c->stream);
-  if (c->accum_stream) (void)hipStreamSynchronize(c->accum_stream);
-  destroy_slots(c);
-  for (auto e : c->slot_done) (void)hipEventDestroy(e);
-  for (auto e : c->slot_free) (void)hipEventDestroy(e);
+  drop_slots(c);  // (each slot drains its stream)
   for (auto& evs : c->pending_ev)
     for (auto e : evs) (void)hipEventDestroy(e);
   for (auto e : c->free_ev) (void)hipEventDestroy(e);
@@ -3174,11 +3201,7 @@ int kdpt_destroy(kdpt_ctx* c) {
   unregister_host(c);
   for (auto e : c->frame_ev)
     if (e) (void)hipEventDestroy(e);
-  for (auto e : c->frame_acc_ev)
-    if (e) (void)hipEventDestroy(e);
   if (c->reduce_stream) (void)hipStreamDestroy(c->reduce_stream);
-  if (c->accum_stream) (void)hipStreamDestroy(c->accum_stream);
-  if (c->accum_ev) (void)hipEventDestroy(c->accum_ev);
   for (void* p : c->allocs) (void)hipFree(p);
   if (c->pbo_staging) (void)hipFree(c->pbo_staging);
   if (c->h_counts) (void)hipHostFree(c->h_counts);
@@ -3684,8 +3707,9 @@ int launch_iteration(kdpt_ctx* c, int iter, int stop_depth, bool count) {
 // kdpt_comm_init, one process per GPU) or, inside one process (kdpt_render_sharded), either RCCL
 // (ncclCommInitAll) or a peer-copy reduce on device 0 that adds the ranks' frames in rank order (also usable
 // with several contexts on one device, which RCCL refuses).  RCCL is loaded at run time (dlopen): the library
-// has no link-time dependency on it, and a process that already holds it (torch) shares that copy.  All
-// reduces are queued on the accumulation streams, so frames stay in flight: frame f + 1's iterations run
+// has no link-time dependency on it, and a process that already holds it (torch) shares that copy.  Each
+// context queues its frames' reduces and rank 0's image adds on a reduce stream of its own, which waits for
+// the frame's last add (the batch streams' add chain), so frames stay in flight: frame f + 1's iterations run
 // while frame f is reduced.
 // ---------------------------------------------------------------------------
 namespace {
@@ -3772,13 +3796,15 @@ void unregister_host(kdpt_ctx* c) {
 
 int frame_buffers(kdpt_ctx* c) {
   const size_t n3 = 3 * (size_t)c->npix;
-  if (!c->reduce_stream) HIP_TRY(hipStreamCreateWithFlags(&c->reduce_stream, hipStreamNonBlocking));
+  if (!c->reduce_stream) {
+    int rc = create_stream(c, &c->reduce_stream);
+    if (rc) return rc;
+  }
   for (int k = 0; k < 2; k++) {
     if (!c->frame_buf[k]) {
       int rc = dalloc(c, &c->frame_buf[k], n3);
       if (rc) return rc;
       HIP_TRY(hipEventCreateWithFlags(&c->frame_ev[k], hipEventDisableTiming));
-      HIP_TRY(hipEventCreateWithFlags(&c->frame_acc_ev[k], hipEventDisableTiming));
       HIP_TRY(hipEventRecord(c->frame_ev[k], c->stream));
     }
   }
@@ -3804,18 +3830,22 @@ void frame_share(int f, int spp, int n, int r, int* first, int* count) {
   *count = r < spp ? (spp - r + n - 1) / n : 0;
 }
 
-// Queue frame f's share of this rank into frame_buf[f & 1] (zeroed first, after its previous reduce).
+// Queue frame f's share of this rank into frame_buf[f & 1] (zeroed first, after its previous reduce), and make
+// the reduce stream wait for it: the share's last add (c->acc_last), or, for a rank with no iterations in the
+// frame, the zeroing itself, done on the reduce stream (which already follows the previous reduce).
 int enqueue_frame(kdpt_ctx* c, int f, int spp, int pipeline, int batch) {
   int rc = frame_buffers(c);
   if (rc) return rc;
-  if (!c->accum_stream) HIP_TRY(hipStreamCreateWithFlags(&c->accum_stream, hipStreamNonBlocking));
   float* fb = c->frame_buf[f & 1];
-  HIP_TRY(hipStreamWaitEvent(c->accum_stream, c->frame_ev[f & 1], 0));
-  HIP_TRY(hipMemsetAsync(fb, 0, sizeof(float) * 3 * (size_t)c->npix, c->accum_stream));
   int first, count;
   frame_share(f, spp, c->nranks, c->rank, &first, &count);
-  if (count > 0) rc = enqueue_iterations(c, first, count, c->nranks, pipeline, batch, fb);
-  return rc;
+  if (count > 0) {
+    if ((rc = enqueue_iterations(c, first, count, c->nranks, pipeline, batch, fb, c->frame_ev[f & 1]))) return rc;
+    HIP_TRY(hipStreamWaitEvent(c->reduce_stream, c->acc_last, 0));
+  } else {
+    HIP_TRY(hipMemsetAsync(fb, 0, sizeof(float) * 3 * (size_t)c->npix, c->reduce_stream));
+  }
+  return KDPT_OK;
 }
 
 // Rank 0, after its frame image is in `sum`: add it into the context's image and copy it out.
@@ -3897,11 +3927,9 @@ int kdpt_render_frames(kdpt_ctx* c, int first_frame, int frames, int spp, int pi
     const int f = first_frame + k;
     if ((rc = enqueue_frame(c, f, spp, pipeline, batch))) return rc;
     float* fb = c->frame_buf[f & 1];
-    // the frame's reduce and image add run on the reduce stream once its accumulations are done, while the
-    // accumulation stream goes on with the next frame's (other buffer)
+    // the frame's reduce and image add run on the reduce stream once its adds are done (enqueue_frame), while
+    // the batch streams go on with the next frame's (other buffer)
     const hipStream_t rs = c->reduce_stream;
-    HIP_TRY(hipEventRecord(c->frame_acc_ev[f & 1], c->accum_stream));
-    HIP_TRY(hipStreamWaitEvent(rs, c->frame_acc_ev[f & 1], 0));
     if ((rc = reduce_spin(c, rs))) return rc;
     const float* sum = fb;
     if (c->external_reduce) {  // the caller reduces: every rank's share goes out as it is
@@ -3915,10 +3943,9 @@ int kdpt_render_frames(kdpt_ctx* c, int first_frame, int frames, int spp, int pi
       if (c->rank == 0 && (rc = finish_frame(c, sum, out, k, rs))) return rc;
     }
     HIP_TRY(hipEventRecord(c->frame_ev[f & 1], rs));
+    // (entry points that read or write the image, and adds into it, follow the last reduce: join_accum)
+    c->img_last = c->frame_ev[f & 1];
   }
-  // whatever follows on the accumulation stream (the next call's accumulations, kdpt_synchronize, entry
-  // points that read the image) follows the last reduce too
-  if (frames > 0) HIP_TRY(hipStreamWaitEvent(c->accum_stream, c->frame_ev[(first_frame + frames - 1) & 1], 0));
   return KDPT_OK;
 }
 
@@ -3978,16 +4005,16 @@ int kdpt_render_sharded(const kdpt_scene* scene, const kdpt_options* opt, int nd
   };
   for (int k = 0; k < frames; k++) {
     const int f = first_frame + k;
-    // each rank queues its share on its accumulation stream; its reduce stream waits for the share (as in
-    // kdpt_render_frames), so frame f + 1's accumulations never queue behind frame f's reduce
+    // each rank queues its share on its batch streams; its reduce stream waits for the share (as in
+    // kdpt_render_frames), so frame f + 1's adds never queue behind frame f's reduce
+    std::vector<hipEvent_t> share_done(ndev, nullptr);  // each rank's last add of the frame (copy reduce)
     for (int i = 0; i < ndev; i++) {
       kdpt_ctx* ci = cs[i];
       if (hipSetDevice(ci->device) != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "hipSetDevice"));
       if ((rc = enqueue_frame(ci, f, spp, pipeline, batch))) return cleanup(rc);
-      if (hipEventRecord(ci->frame_acc_ev[f & 1], ci->accum_stream) != hipSuccess ||
-          hipStreamWaitEvent(ci->reduce_stream, ci->frame_acc_ev[f & 1], 0) != hipSuccess)
-        return cleanup(fail(KDPT_ERR_HIP, "frame events"));
       if ((rc = reduce_spin(ci, ci->reduce_stream))) return cleanup(rc);
+      // (recorded on the rank's reduce stream, which already waits for the share)
+      if (!xevent(ci->device, ci->reduce_stream, &share_done[i])) return cleanup(fail(KDPT_ERR_HIP, "frame events"));
     }
     if (hipSetDevice(c0->device) != hipSuccess) return cleanup(fail(KDPT_ERR_HIP, "hipSetDevice"));
     if ((rc = frame_buffers(c0))) return cleanup(rc);
@@ -4009,7 +4036,7 @@ int kdpt_render_sharded(const kdpt_scene* scene, const kdpt_options* opt, int nd
       for (int i = 1; i < ndev; i++) {
         kdpt_ctx* ci = cs[i];
         if (hipSetDevice(c0->device) != hipSuccess ||
-            hipStreamWaitEvent(c0->reduce_stream, ci->frame_acc_ev[f & 1], 0) != hipSuccess ||
+            hipStreamWaitEvent(c0->reduce_stream, share_done[i], 0) != hipSuccess ||
             hipMemcpyPeerAsync(staged[i], c0->device, ci->frame_buf[f & 1], ci->device, sizeof(float) * (size_t)n3,
                                c0->reduce_stream) != hipSuccess)
           return cleanup(fail(KDPT_ERR_HIP, "copy reduce"));

@@ -120,6 +120,13 @@ EXPORTS = [
 
 REDUCE_RCCL, REDUCE_COPY = 0, 1  # kdpt_render_sharded's reduce (KDPT_REDUCE_*)
 
+
+def set_process_tuning(name: str, value: float):
+    """kdpt_set_tuning(NULL, ...): a process-wide knob that contexts created afterwards start with
+    ("reduce_spin_us", "cluster_chord")."""
+    lib = load_library()
+    _check(lib.kdpt_set_tuning(None, name.encode(), float(value)), f"kdpt_set_tuning(NULL, {name})")
+
 _lib = None
 
 
@@ -163,7 +170,7 @@ def load_library(path: str = LIB_PATH) -> C.CDLL:
     if hasattr(lib, "kdpt_cull_margin"):  # absent from older builds used in A/B runs
         lib.kdpt_cull_margin.argtypes = [C.c_void_p, P(C.c_float), P(C.c_double), P(C.c_int)]
     if hasattr(lib, "kdpt_cull_masks"):
-        lib.kdpt_cull_masks.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), C.c_void_p, C.c_void_p]
+        lib.kdpt_cull_masks.argtypes = [C.c_void_p, P(C.c_int), P(C.c_int), C.c_void_p]
     if hasattr(lib, "kdpt_render_frames"):
         lib.kdpt_comm_unique_id.argtypes = [C.c_void_p]
         lib.kdpt_comm_init.argtypes = [C.c_void_p, C.c_int, C.c_int, C.c_void_p]
@@ -521,18 +528,15 @@ class PathTracer:
         return {"cull_margin": k.value, "cull_rigorous": r.value, "cull_exact": bool(e.value)}
 
     def cull_masks(self):
-        """kdpt_cull_masks: (mask_n, masks, codes) of the masked cull as the device built them, bucket-major arrays
-        of shape [6 mask_n^2, num_clusters]; (0, None, None) when the scene has none."""
+        """kdpt_cull_masks: (mask_n, masks) of the masked cull as the device built them, a bucket-major array of
+        shape [6 mask_n^2, num_clusters]; (0, None) when the scene has none."""
         n, ncl = C.c_int(), C.c_int()
-        _check(self.lib.kdpt_cull_masks(self._ctx, C.byref(n), C.byref(ncl), None, None), "kdpt_cull_masks")
+        _check(self.lib.kdpt_cull_masks(self._ctx, C.byref(n), C.byref(ncl), None), "kdpt_cull_masks")
         if n.value == 0:
-            return 0, None, None
-        cells = (6 * n.value * n.value, ncl.value)
-        masks = np.zeros(cells, np.uint64)
-        codes = np.zeros(cells, np.uint8)
-        _check(self.lib.kdpt_cull_masks(self._ctx, C.byref(n), C.byref(ncl), masks.ctypes.data, codes.ctypes.data),
-               "kdpt_cull_masks")
-        return n.value, masks, codes
+            return 0, None
+        masks = np.zeros((6 * n.value * n.value, ncl.value), np.uint64)
+        _check(self.lib.kdpt_cull_masks(self._ctx, C.byref(n), C.byref(ncl), masks.ctypes.data), "kdpt_cull_masks")
+        return n.value, masks
 
     def trace_grid_share(self) -> float:
         return float(self.stats().intersect_grid_share)

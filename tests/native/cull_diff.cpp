@@ -186,32 +186,23 @@ double bound_ratio(f3 o, f3 d, float4 v0, float4 e1, float4 e2, float bx, float 
 }
 
 // The product's masked cull (kdpt_device.h trace_phase, one-level route) for a (line, cluster) pair whose line
-// missed the cluster's fast-margin box or oriented box: the pair's cell (dir_bucket) and its bound code; when
-// the line meets the box widened by mask_bound(code) (or the kernel reads every mask: knob "cull_bound" = 0), the
-// danger mask's triangles that danger_needs_test keeps (those get glm's u/v tests).  `loaded`: the pair's 8-byte
-// mask was read.
+// missed the cluster's fast-margin box or oriented box: the pair's cell (dir_bucket) and its danger mask, and the
+// mask's triangles that danger_needs_test keeps (those get glm's u/v tests).
 struct MaskTables {
   int n = 0, ncl = 0;
   float c = 0.0f;
   std::vector<unsigned long long> masks;  // bucket-major, DevScene::cl_mask
-  std::vector<unsigned char> codes;       // DevScene::cl_mq
   std::vector<float4> tn;                 // DevScene::cl_tn
   void build(const ClusterSet& cs, int res, float Kf, float cc) {
     n = res;
     ncl = (int)cs.info.size();
     c = cc;
-    build_dir_masks(cs, n, Kf, masks, codes);
+    build_dir_masks(cs, n, Kf, masks);
     build_entry_normals(cs, tn);
   }
-  // bound: the kernel's "cull_bound" route (the cell's code checked before the mask is read)
-  unsigned long long needs(bool bound, int cl, float4 L, float4 H, f3 o, f3 inv, f3 d, bool& loaded,
-                           int& items) const {
-    const uint32_t mi = (uint32_t)dir_bucket(d, n) * (uint32_t)ncl + (uint32_t)cl;
-    const uint32_t q = bound ? codes[mi] : 255u;
-    loaded = q != 0u && (q == 255u || cluster_may_pass(L, H, o, inv, mask_bound(q)));
+  unsigned long long needs(int cl, float4 L, float4 H, f3 o, f3 inv, f3 d, int& items) const {
+    unsigned long long m = masks[(size_t)dir_bucket(d, n) * ncl + cl], nm = 0ull;
     items = 0;
-    if (!loaded) return 0ull;
-    unsigned long long m = masks[mi], nm = 0ull;
     const float D = box_miss(L, H, o, inv);
     while (m) {
       const int k = __builtin_ctzll(m);
@@ -221,23 +212,16 @@ struct MaskTables {
     }
     return nm;
   }
-  // the same with kd_rcp's quotient moved by -1, 0 and +1 ulp (v_rcp_f32's error), and with and without the
-  // bound codes: the triangles kept under every one of them (a pass must be kept under each); stats from the
-  // unperturbed product route
-  unsigned long long needs_all(bool bound, int cl, float4 L, float4 H, f3 o, f3 inv, f3 d, bool& loaded,
-                               int& items) const {
+  // the same with kd_rcp's quotient moved by -1, 0 and +1 ulp (v_rcp_f32's error): the triangles kept under
+  // every one of them (a pass must be kept under each); the item count of the unperturbed one
+  unsigned long long needs_all(int cl, float4 L, float4 H, f3 o, f3 inv, f3 d, int& items) const {
     unsigned long long all = ~0ull;
-    for (int bnd : {1, 0})
-      for (int p : {0, -1, 1}) {
-        kdpt_rcp_ulp = p;
-        bool ld;
-        int it;
-        all &= needs(bnd != 0, cl, L, H, o, inv, d, ld, it);
-        if (p == 0 && (bnd != 0) == bound) {
-          loaded = ld;
-          items = it;
-        }
-      }
+    for (int p : {0, -1, 1}) {
+      kdpt_rcp_ulp = p;
+      int it;
+      all &= needs(cl, L, H, o, inv, d, it);
+      if (p == 0) items = it;
+    }
     kdpt_rcp_ulp = 0;
     return all;
   }
@@ -246,8 +230,8 @@ struct MaskTables {
 // Cull statistics of real rays through the traversal (--sim): each ray walks the tree (traverseKD, compiled
 // here for the host); for every big leaf it tests, every cluster of the leaf is evaluated with the fast cull (box
 // at the scene margin + oriented box at cull_margin_dir) and with the product's masked cull (box and oriented
-// box at the masked cull's coefficient Kf; a missed pair's bound code, mask and danger_needs_test, under each
-// of the three reciprocal perturbations).  A pair a cull drops while a triangle passes glm's u/v tests, or a
+// box at the masked cull's coefficient Kf; a missed pair's mask and danger_needs_test, under each of the three
+// reciprocal perturbations).  A pair a cull drops while a triangle passes glm's u/v tests, or a
 // passing triangle the masked cull does not test, is a violation.
 int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_bare* tris, int nt,
         const std::vector<float4>& tv, const std::vector<float4>& e1, const std::vector<float4>& e2,
@@ -288,12 +272,11 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
   S.n0_left = nodes[0].leftID; S.n0_right = nodes[0].rightID;
   S.n1_left = nn > 1 ? nodes[1].leftID : -1; S.n1_right = nn > 1 ? nodes[1].rightID : -1;
   long long leaves = 0, pairs = 0, old_sw = 0, msk_sw = 0, prod = 0, viol_old = 0, nofast = 0, small_tris = 0,
-            old_tris = 0, msk_missed = 0, msk_loads = 0, msk_items = 0, viol_msk = 0, msk_needed = 0;
+            old_tris = 0, msk_missed = 0, msk_nonzero = 0, msk_items = 0, viol_msk = 0, msk_needed = 0;
   const float KF = mask_kf();
-  const bool bound = !getenv("MASK_BOUND") || atoi(getenv("MASK_BOUND")) != 0;  // stats of that route
   MaskTables mt;
   mt.build(cs, mask_res((int)cs.info.size()), KF, cm.c);
-#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, pairs, old_sw, msk_sw, prod, viol_old, nofast, small_tris, old_tris, msk_missed, msk_loads, msk_items, viol_msk, msk_needed)
+#pragma omp parallel for schedule(dynamic, 256) reduction(+ : leaves, pairs, old_sw, msk_sw, prod, viol_old, nofast, small_tris, old_tris, msk_missed, msk_nonzero, msk_items, viol_msk, msk_needed)
   for (long long i = 0; i < nr; i++) {
     const f3 o = mk3(r[6 * i], r[6 * i + 1], r[6 * i + 2]), d = mk3(r[6 * i + 3], r[6 * i + 4], r[6 * i + 5]);
     const f3 inv = mk3(1.0f / d.x, 1.0f / d.y, 1.0f / d.z);
@@ -345,10 +328,9 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
           continue;
         }
         msk_missed++;
-        bool loaded;
         int items;
-        const unsigned long long nm = mt.needs_all(bound, c, L, H, o, inv, d, loaded, items);
-        msk_loads += loaded;
+        const unsigned long long nm = mt.needs_all(c, L, H, o, inv, d, items);
+        msk_nonzero += items > 0;
         msk_items += items;
         msk_needed += __builtin_popcountll(nm);
         viol_msk += (passes & ~nm) != 0ull;
@@ -359,9 +341,9 @@ int sim(const char* path, const kdpt_node_bare* nodes, int nn, const kdpt_tri_ba
   printf("{\"rays\": %lld, \"clusters\": %zu, \"mode\": %d, \"chord\": %g, \"big_leaves_per_ray\": %.4f, "
          "\"pairs_per_ray\": %.4f, \"sweeps_old\": %.4f, \"sweeps_masked\": %.4f, \"productive\": %.4f, "
          "\"viol_old\": %lld, \"nofast\": %lld, \"small_tris\": %.3f, \"old_tris\": %.3f, \"mask_n\": %d, "
-         "\"msk_missed\": %.4f, \"msk_loads\": %.4f, \"msk_items\": %.4f, \"msk_needed\": %.4f, \"viol_msk\": %lld}\n",
+         "\"msk_missed\": %.4f, \"msk_nonzero\": %.4f, \"msk_items\": %.4f, \"msk_needed\": %.4f, \"viol_msk\": %lld}\n",
          nr, cs.info.size(), grp.mode, grp.chord, leaves / R, pairs / R, old_sw / R, msk_sw / R, prod / R, viol_old,
-         nofast, small_tris / R, old_tris / R, mt.n, msk_missed / R, msk_loads / R, msk_items / R, msk_needed / R,
+         nofast, small_tris / R, old_tris / R, mt.n, msk_missed / R, msk_nonzero / R, msk_items / R, msk_needed / R,
          viol_msk);
   return 0;
 }
@@ -395,29 +377,24 @@ int main(int argc, char** argv) {
     e2[i] = make_float4(T.x3 - T.x1, T.y3 - T.y1, T.z3 - T.z1, 0.0f);
   }
   if (strcmp(argv[2], "--masks") == 0) {
-    // cull_diff TREE --masks OUT.bin: the masks and bound codes kdpt_create builds on the device for this tree
-    // (the scene's masked-cull coefficient and resolution), from the host builder: int32 n, int32 num_clusters,
-    // float Kf, uint64 masks[6 n^2][num_clusters], uint8 codes[6 n^2][num_clusters]
+    // cull_diff TREE --masks OUT.bin: the masks kdpt_create builds on the device for this tree (the scene's
+    // masked-cull coefficient and resolution), from the host builder: int32 n, int32 num_clusters, float Kf,
+    // uint64 masks[6 n^2][num_clusters]
     ClusterSet cs;
     build_cluster_set(nodes.data(), nn, tris.data(), tv, e1, e2, cs);
     const CullMargin cm = cluster_margin(cs.cv0, cs.ce1, cs.ce2);
     const int n = mask_res((int)cs.info.size()), ncl = (int)cs.info.size();
     std::vector<unsigned long long> masks;
-    std::vector<unsigned char> codes;
-    build_dir_masks(cs, n, cm.K, masks, codes);
+    build_dir_masks(cs, n, cm.K, masks);
     FILE* g = fopen(argv[3], "wb");
     if (!g) return 3;
     const bool ok = fwrite(&n, 4, 1, g) == 1 && fwrite(&ncl, 4, 1, g) == 1 && fwrite(&cm.K, 4, 1, g) == 1 &&
-                    fwrite(masks.data(), 8, masks.size(), g) == masks.size() &&
-                    fwrite(codes.data(), 1, codes.size(), g) == codes.size();
+                    fwrite(masks.data(), 8, masks.size(), g) == masks.size();
     fclose(g);
-    long long nz = 0, coded = 0;
-    for (size_t k = 0; k < masks.size(); k++) {
-      nz += masks[k] != 0ull;
-      coded += codes[k] != 0;
-    }
-    printf("{\"n\": %d, \"clusters\": %d, \"kf\": %.9g, \"exact\": %d, \"nonzero\": %lld, \"coded\": %lld, \"cells\": %zu}\n",
-           n, ncl, (double)cm.K, (int)cm.exact, nz, coded, masks.size());
+    long long nz = 0;
+    for (size_t k = 0; k < masks.size(); k++) nz += masks[k] != 0ull;
+    printf("{\"n\": %d, \"clusters\": %d, \"kf\": %.9g, \"exact\": %d, \"nonzero\": %lld, \"cells\": %zu}\n",
+           n, ncl, (double)cm.K, (int)cm.exact, nz, masks.size());
     return ok ? 0 : 3;
   }
   if (strcmp(argv[2], "--sim") == 0) {
@@ -612,9 +589,8 @@ int main(int argc, char** argv) {
                          cluster_may_pass_obb_k(L, H, cs.nrm[c], cs.obb_u[c], cs.obb_v[c], cs.obb_w[c], of, inv, df, ndv,
                                                 KF);
         if (!hit) {
-          bool loaded;
           int items;
-          const unsigned long long nm = mt.needs_all(true, c, L, H, of, inv, df, loaded, items);
+          const unsigned long long nm = mt.needs_all(c, L, H, of, inv, df, items);
           C.mask_items += items;
           C.mask_needed += __builtin_popcountll(nm);
           for (int k = 0; k < inf.y; k++) {

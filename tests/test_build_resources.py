@@ -51,11 +51,9 @@ HOT = {"k_traceILb1ELb0ELi2E": 4, "k_traceILb0ELb0ELi2E": 4, "k_traceILb1ELb0ELi
 # pass's sweeps, two normal records per trip) keeps the mask live across the sweep: +4 B on the LDS-tree route C3
 # runs (mode 2), +30-40 B on the derived-record routes (modes 3 / 4) that carry the masked cull for larger trees;
 # the C5 route (mode 5, no masks) is unchanged.  Measured with the spills: profiles/r05_ab_log.md.
-# Round 6's bound codes (the cell's code read with the box test, the mask requested only when the line meets the
-# box widened by the code's bound) add 8-16 B on modes 2-4 (profiles/r06_ab_log.md).
-SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 44, "k_traceILb0ELb0ELi2E": 44, "k_traceILb1ELb0ELi3E": 116,
-              "k_traceILb0ELb0ELi3E": 116, "k_traceILb1ELb0ELi4E": 104,
-              "k_traceILb0ELb0ELi4E": 104, "k_traceILb1ELb0ELi5E": 116, "k_traceILb0ELb0ELi5E": 116,
+SCRATCH_OK = {"k_traceILb1ELb0ELi2E": 40, "k_traceILb0ELb0ELi2E": 40, "k_traceILb1ELb0ELi3E": 104,
+              "k_traceILb0ELb0ELi3E": 104, "k_traceILb1ELb0ELi4E": 92,
+              "k_traceILb0ELb0ELi4E": 92, "k_traceILb1ELb0ELi5E": 116, "k_traceILb0ELb0ELi5E": 116,
               "k_shade_fused": 28}
 
 

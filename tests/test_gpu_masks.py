@@ -2,7 +2,7 @@
 cost of (re)creating a context, which the drop-in shim pays on every camera move (src/main.cpp:1134-1137 calls
 pathtraceFree + pathtraceInit).
 
-- The device-built danger masks and bound codes equal the host builder's (kdpt_clusters.h build_dir_masks, the
+- The device-built danger masks equal the host builder's (kdpt_clusters.h build_dir_masks, the
   tables the host harness tests/native/cull_diff.cpp proves exact) cell for cell, at the shipped resolution and
   after a knob rebuilds them.
 - Rebuilding them (knobs "cull_mask_n", "cull_fast_k") frees the previous tables.
@@ -49,32 +49,28 @@ def _host_masks(cull_diff, sd, path, n=None):
     info = json.loads(r.stdout.strip().splitlines()[-1])
     raw = open(path, "rb").read()
     n_, ncl, _ = struct.unpack("<iif", raw[:12])
-    cells = 6 * n_ * n_ * ncl
-    masks = np.frombuffer(raw, np.uint64, cells, 12).reshape(6 * n_ * n_, ncl)
-    codes = np.frombuffer(raw, np.uint8, cells, 12 + 8 * cells).reshape(6 * n_ * n_, ncl)
-    return info, n_, masks, codes
+    masks = np.frombuffer(raw, np.uint64, 6 * n_ * n_ * ncl, 12).reshape(6 * n_ * n_, ncl)
+    return info, n_, masks
 
 
 def test_device_masks_equal_host_builder(kdpt, cull_diff, tmp_path):
-    """dragon_5 (C3's mesh): the 6 * 128^2 * 181 cells the device builds equal the host builder's, masks and
-    bound codes; most cells are empty (bound code 0), and every non-empty mask has a code."""
+    """dragon_5 (C3's mesh): the 6 * 128^2 * 181 cells the device builds equal the host builder's, bit for bit;
+    most cells are empty."""
     desc = load_fixture_scene("cornell", "dragon_5", res=(64, 48), depth=8)
     sd = kdpt.SceneData.from_description(desc)
-    info, n, hm, hq = _host_masks(cull_diff, sd, str(tmp_path / "m128.bin"))
+    info, n, hm = _host_masks(cull_diff, sd, str(tmp_path / "m128.bin"))
     with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
-        dn, dm, dq = pt.cull_masks()
+        dn, dm = pt.cull_masks()
         assert dn == n == 128, (dn, info)
         assert np.array_equal(dm, hm)
-        assert np.array_equal(dq, hq)
-        assert ((dm != 0) == (dq != 0)).all()
-        assert 0.1 < (dq != 0).mean() < 0.6, (dq != 0).mean()
+        assert 0.1 < (dm != 0).mean() < 0.6, (dm != 0).mean()
         assert pt.stats().mask_build_ms > 0
-        # rebuilt by the knobs at another resolution and box coefficient: still the host builder's cells
+        # rebuilt by the knob at another resolution: still the host builder's cells
         pt.set_tuning("cull_mask_n", 32)
-        _, n32, hm32, hq32 = _host_masks(cull_diff, sd, str(tmp_path / "m32.bin"), 32)
-        dn, dm, dq = pt.cull_masks()
+        _, n32, hm32 = _host_masks(cull_diff, sd, str(tmp_path / "m32.bin"), 32)
+        dn, dm = pt.cull_masks()
         assert dn == n32 == 32
-        assert np.array_equal(dm, hm32) and np.array_equal(dq, hq32)
+        assert np.array_equal(dm, hm32)
 
 
 def test_mask_rebuilds_free_the_previous_tables(kdpt):
@@ -98,7 +94,8 @@ def test_mask_rebuilds_free_the_previous_tables(kdpt):
 def test_create_time_on_c3(kdpt):
     """kdpt_create on C3 (cornell + dragon_5, 800x800, depth 8) with the masks built on the device: the host
     wall time kdpt_stats reports for a context created after the process's first (as the shim re-creates one on
-    every camera move) stays within 100 ms, and the masks take a small part of it."""
+    every camera move) stays within 50 ms (measured 4-5 ms, of which the masks 2.4), and the masks take a small part
+    of it."""
     desc = load_fixture_scene("cornell", "dragon_5", res=(800, 800), depth=8)
     sd = kdpt.SceneData.from_description(desc)
     times = []
@@ -108,4 +105,4 @@ def test_create_time_on_c3(kdpt):
             times.append((st.create_ms, st.mask_build_ms))
     print("create_ms, mask_build_ms:", times)
     assert all(m > 0 for _, m in times)
-    assert min(t for t, _ in times[1:]) < 100.0, times
+    assert max(t for t, _ in times[1:]) < 50.0, times

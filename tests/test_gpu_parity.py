@@ -320,8 +320,7 @@ def test_tuning_knobs_keep_parity(kdpt):
                       ("chunk_width1", 8), ("trace_grid_frac", 0.1), ("shade_fused", 0), ("shade_batch", 0),
                       ("gen_geoms", 0), ("cluster_cull", 0), ("cull_margin", 1e-3), ("cluster_obb", 0),
                       ("super_slab", 0), ("flat_obb", 0), ("cull_exact", 0), ("cull_mask_n", 8),
-                      ("cull_mask_n", 2), ("cull_mask_n", 32), ("cull_fast_k", 1e-4), ("cull_fast_k", 1e-2),
-                      ("cull_bound", 0)):
+                      ("cull_mask_n", 2), ("cull_mask_n", 32), ("cull_fast_k", 1e-4), ("cull_fast_k", 1e-2)):
         with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
             pt.set_tuning(name, val)
             pt.trace_iterations(1, 8, pipeline=2, batch=4)

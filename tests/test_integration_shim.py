@@ -104,7 +104,7 @@ def test_shim_reinit_on_camera_move_equals_oracle(shim_driver, oracle, tmp_path)
     info = __import__("json").loads(r.stdout.strip().splitlines()[-1])
     print("pathtraceInit ms:", info["init_ms"])
     assert len(info["init_ms"]) == 3
-    assert max(info["init_ms"][1:]) < 100.0, info
+    assert max(info["init_ms"][1:]) < 50.0, info
     img = np.fromfile(out, np.float32).reshape(72, 96, 3)
     s = oracle.OracleScene.from_files(scene, obj, res=(96, 72))
     ref, _ = s.render(1, 2)

@@ -27,6 +27,7 @@ ap.add_argument("--queues", type=int, default=None)
 ap.add_argument("--spin", type=float, default=5000.0)
 ap.add_argument("--frames", type=int, nargs=2, default=(8, 88))
 ap.add_argument("--spp", type=int, default=32)
+ap.add_argument("--cu-mask", action="store_true", help="contexts' batch / reduce streams with an all-CU mask")
 a = ap.parse_args()
 if a.queues:
     os.environ["GPU_MAX_HW_QUEUES"] = str(a.queues)
@@ -66,7 +67,10 @@ def per_frame_sharded(spin):
 
 
 lib.kdpt_set_tuning.argtypes = [C.c_void_p, C.c_char_p, C.c_double]
-out = {"queues": os.environ.get("GPU_MAX_HW_QUEUES", "default"), "spin_us": a.spin, "spp": a.spp}
+if a.cu_mask:
+    kdpt.set_process_tuning("cu_mask_streams", 1)
+out = {"queues": os.environ.get("GPU_MAX_HW_QUEUES", "default"), "spin_us": a.spin, "spp": a.spp,
+       "cu_mask_streams": a.cu_mask}
 A = kdpt.PathTracer(sd, opt, device=0)
 per_frame_ctx(A, 0)  # warm
 out["A_first"] = {"spin0": per_frame_ctx(A, 0), "spin": per_frame_ctx(A, a.spin)}
