@@ -250,9 +250,12 @@ int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
  * are rebuilt for it), "reduce_spin_us" (0; > 0: a device spin of that many
  * microseconds on the reduce stream before every frame's reduce, emulating an ncclReduce that waits for a slower
  * peer -- a diagnostic of the frame pipeline; ctx = NULL sets it for contexts created later, e.g. the ones
- * kdpt_render_sharded creates), "sync_debug" (0).  ctx = NULL only: "cluster_chord" (-1 = the default grouping;
- * > 0: contexts created later group every big leaf's triangles into normal cones of that chord before the Morton
- * runs -- an A/B of the cluster layout; the results are the same bits).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots
+ * kdpt_render_sharded creates), "sync_debug" (0).  ctx = NULL only (process defaults of the contexts created afterwards):
+ * "cluster_chord" (-1: normal cones of chord 0.02 before the Morton runs for meshes whose cull margin is
+ * rigorous, Morton runs only otherwise; 0: Morton runs only; > 0: cones of that chord for every mesh -- the
+ * cluster layout, same bits), "cu_mask_streams" (1: the context's streams are created with a mask of every CU,
+ * each on a hardware queue of its own; 0: plain non-blocking streams, which HIP multiplexes onto
+ * GPU_MAX_HW_QUEUES in-order queues).  KDPT_ERR_ARG for an unknown name.  Drops the pipeline slots
  * (they are remade). */
 int kdpt_set_tuning(kdpt_ctx *ctx, const char *name, double value);
 /* The intersect kernel's configuration: tree source (0 HBM 64-byte records, 1 HBM 32-byte, 2 LDS 32-byte,

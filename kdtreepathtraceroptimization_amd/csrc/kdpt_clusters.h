@@ -75,6 +75,7 @@ struct ClusterGrouping {
 };
 
 constexpr double ULP_HALF = 5.9604644775390625e-8;  // u = 2^-24
+constexpr double CLUSTER_CHORD_EXACT = 0.03;  // the normal-cone chord of meshes whose cull margin is rigorous
 
 // The exact cull's coefficients of one cluster (ClusterSet::kc, read by cull_k_exact), from the triangles glm
 // tests (v0, e1, e2 as floats; products exact in double):

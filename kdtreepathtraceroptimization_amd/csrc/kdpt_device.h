@@ -111,6 +111,9 @@ struct DevScene {
   // cluster padded to CLUSTER entries (cluster c = entries [CLUSTER c, CLUSTER (c + 1)); padding: zeros, index -1)
   const int2* leaf_cl;
   int num_clusters;
+  // 1 when some big leaf has more clusters than ceil(size / CLUSTER) (normal-cone grouping: balanced runs per
+  // cone), so the kernels read each leaf's count from leaf_cl instead of deriving it from the leaf's size
+  int cl_counts;
   const float4* cl_lo;
   const float4* cl_hi;
   const int2* cl_info;
@@ -1241,7 +1244,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
   // the leaf's own record, read once here rather than carried through every node trip (a lane that reaches
   // a leaf neither climbs nor descends, so cur is the leaf)
   const int lnode = cur;
-  int lstart = 0, lsize = 0, lparent = -1;
+  int lstart = 0, lsize = 0, lparent = -1, lclusters = 0;
   uint32_t lkc = 7u;
   float lrestore = 0.0f;
   if (leaf) {
@@ -1253,6 +1256,10 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
       lkc = ln.kc;
       lrestore = ln.restore;
     }
+    // a big leaf's cluster count: Morton runs of CLUSTER fill all but the last, unless the scene groups by
+    // normal cones (S.cl_counts: the count from leaf_cl, requested here, read at the leaf phase)
+    lclusters = (lsize + CLUSTER - 1) / CLUSTER;
+    if (S.cl_counts && lsize >= BIG_LEAF) lclusters = S.leaf_cl[lnode].y;
   }
   // ---------------- leaf phase (wave-cooperative) ----------------
   // per lane results of this phase
@@ -1274,7 +1281,7 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     // Sweeps of the (ray, cluster) pairs `pass` marks: cluster c with the ray of lane own, each surviving
     // cluster by the whole wave, the next survivor's triangles fetched while this one is tested; the results
     // are folded into the owner lane's k_* (order-free).  Wave-uniform call.
-    auto sweep64 = [&](bool pass, int c, int own, auto&& mid) {
+    auto sweep64 = [&](bool pass, int c, int own) {
       unsigned long long sm = __ballot(pass);
       int s = -1;
       TriData T{};
@@ -1284,7 +1291,6 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         const int ct = __builtin_amdgcn_readlane(c, s) * 64 + lane;
         T = TriData{S.c_v0[ct], S.c_e1[ct], S.c_e2[ct]};
       }
-      mid();  // (after the first survivor's loads: vector loads complete in issue order)
       while (s >= 0) {
         int sn = -1;
         TriData Tn{};
@@ -1427,9 +1433,9 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
     };
     auto sweep = [&](bool pass, int c, int own) {
       if constexpr (CLUSTER == 32) sweep32(pass, c, own);
-      else sweep64(pass, c, own, [] {});
+      else sweep64(pass, c, own);
     };
-    const int ncl = big ? (lsize + CLUSTER - 1) / CLUSTER : 0;
+    const int ncl = big ? lclusters : 0;
     if constexpr (ClusterSrc::kSuper) {
       // Two levels (leaves of thousands of triangles, e.g. the C5 icosphere's): the (ray, super-cluster) pairs
       // are culled first, 64 per pass, against the supers' boxes (LDS); each surviving super's SUPER clusters
@@ -1562,9 +1568,6 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
         const int c = W->tbase[own] + B + lane;
         bool hit = B + lane < P;  // (no cull: every pair swept)
         unsigned long long m = 0ull;  // a missed pair's danger mask (exact cull)
-#ifdef KDPT_MASK_MID
-        uint32_t mmi = 0u;  // (A/B) the missed pair's cell + 1: its mask is read once the sweep's first loads are out
-#endif
         if (fastAABB) {
           const float4 od = W->od[own];  // the pair's ray from the wave's LDS copy (wave_ray_start)
           const float2 d2 = W->dd[own];
@@ -1572,15 +1575,9 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
           float4 clo = make_float4(0.0f, 0.0f, 0.0f, 0.0f), chi = clo;
           unsigned long long dm = 0ull;
-          uint32_t mi = 0u;  // the pair's (bucket, cluster) cell (exact cull)
           const bool valid = hit;
           if (valid) {
-            if (exact) {
-              mi = (uint32_t)dir_bucket(dd, S.mask_n) * (uint32_t)S.num_clusters + (uint32_t)c;
-#ifndef KDPT_MASK_MID
-              dm = S.cl_mask[mi];
-#endif
-            }
+            if (exact) dm = S.cl_mask[(uint32_t)dir_bucket(dd, S.mask_n) * (uint32_t)S.num_clusters + (uint32_t)c];
             clo = clusters.lo_of(c);
             chi = clusters.hi_of(c);
             hit = cluster_may_pass(clo, chi, oo, ii, S.cl_margin);
@@ -1593,20 +1590,10 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
                                            cn.x * dd.x + cn.y * dd.y + cn.z * dd.z, S.cl_margin);
             }
           }
-#ifdef KDPT_MASK_MID
-          if (exact && valid && !hit) mmi = mi + 1u;
-#else
           if (exact && valid && !hit) m = dm;
-#endif
         }
         if (COUNT) prof_lap(WP, PROF_BIG_CULL_CYC);
-#ifdef KDPT_MASK_MID
-        sweep64(hit, c, own, [&] {
-          if (mmi) m = S.cl_mask[mmi - 1u];
-        });
-#else
         sweep(hit, c, own);
-#endif
         if (COUNT) prof_lap(WP, PROF_BIG_CYC);
         if (!exact || !__any(m != 0ull)) continue;
         bool late = false;  // a danger triangle passed glm's u/v tests: sweep the cluster now

@@ -48,7 +48,7 @@ constexpr int MAX_KEYS = 64;
 thread_local std::string g_last_error;
 double g_reduce_spin_us = 0;  // kdpt_set_tuning(NULL, "reduce_spin_us", v): the default of new contexts
 double g_cluster_chord = -1;   // kdpt_set_tuning(NULL, "cluster_chord", v): big-leaf grouping of new contexts
-bool g_cu_mask_streams = false;  // kdpt_set_tuning(NULL, "cu_mask_streams", 1): ... and their stream kind
+bool g_cu_mask_streams = true;  // kdpt_set_tuning(NULL, "cu_mask_streams", v): ... and their stream kind
 
 int fail(int code, const std::string& msg) {
   g_last_error = msg;
@@ -1777,9 +1777,12 @@ struct kdpt_ctx {
 
 namespace {
 
-// A stream for the batches and the frame reduces: non-blocking, or (knob "cu_mask_streams", A/B) one created with
-// a mask of every CU -- such a stream gets a hardware queue of its own instead of one of the GPU_MAX_HW_QUEUES
-// (4 by default) that HIP multiplexes the process's other streams onto.
+// A context's streams (its own, the batch groups' and the frame reduce's): created with a mask of every CU, which
+// gives each a hardware queue of its own instead of one of the GPU_MAX_HW_QUEUES (4 by default) in-order queues
+// HIP multiplexes a process's plain streams onto -- where a waiting or long-running command of one stream holds
+// the others on its queue.  C4's 32-spp frames: 6.49 -> 5.68 ms with 24 queues, and a 5 ms reduce delay per frame
+// costs nothing at 4 or 24 queues (profiles/r06_ab_log.md).  Knob "cu_mask_streams" = 0 (process default):
+// plain non-blocking streams; a failed creation falls back to one.
 int create_stream(kdpt_ctx* c, hipStream_t* st) {
   if (c->cu_mask_streams) {
     hipDeviceProp_t prop;
@@ -1787,8 +1790,8 @@ int create_stream(kdpt_ctx* c, hipStream_t* st) {
     const int n = std::max(1, prop.multiProcessorCount);
     std::vector<uint32_t> mask((n + 31) / 32, 0xffffffffu);
     if (n % 32) mask.back() = (1u << (n % 32)) - 1u;
-    HIP_TRY(hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()));
-    return KDPT_OK;
+    if (hipExtStreamCreateWithCUMask(st, (uint32_t)mask.size(), mask.data()) == hipSuccess) return KDPT_OK;
+    (void)hipGetLastError();
   }
   HIP_TRY(hipStreamCreateWithFlags(st, hipStreamNonBlocking));
   return KDPT_OK;
@@ -2113,12 +2116,24 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
                    const std::vector<float4>& e2, std::vector<int2>& leaf_cl, std::vector<int2>& leaf_sp) {
   ClusterSet cs;
   build_cluster_set(sc->nodes, sc->num_nodes, sc->tris, tv, e1, e2, cs);
-  // (A/B: "cluster_chord" > 0 groups every big leaf's triangles by normal cones of that chord first)
-  if (g_cluster_chord > 0) {
-    ClusterGrouping g;
-    g.mode = 1;
-    g.chord = g_cluster_chord;
-    build_cluster_set(sc->nodes, sc->num_nodes, sc->tris, tv, e1, e2, cs, g);
+  // Meshes of small triangles (a rigorous margin: the two-level cull of the C5 icosphere) group each big leaf's
+  // triangles into normal cones of chord CLUSTER_CHORD_EXACT first, then Morton runs per cone: flatter clusters
+  // whose oriented boxes the lines miss more often -- C5's sweeps per ray 1.83 -> 1.30 (host simulation), C5
+  // 4 568 / 4 377 -> 5 110 / 5 087 Mrays/s (profiles/r06_ab_log.md).  Only the order of a leaf's sweeps changes
+  // (the results fold order-free); such leaves hold more clusters than ceil(size / 64) (S.cl_counts).  Not for meshes of large triangles: dragon_5's leaves split into 4-8x as many
+  // clusters.  Kept only while the super-clusters grow by at most 40 % (they must fit the LDS route); knob
+  // "cluster_chord" (process default): 0 = Morton runs only, > 0 = that chord for every mesh.
+  {
+    const double chord = g_cluster_chord >= 0 ? g_cluster_chord
+                                             : (cluster_margin(cs.cv0, cs.ce1, cs.ce2).exact ? CLUSTER_CHORD_EXACT : 0.0);
+    if (chord > 0 && !cs.info.empty()) {
+      ClusterGrouping g;
+      g.mode = 1;
+      g.chord = chord;
+      ClusterSet cones;
+      build_cluster_set(sc->nodes, sc->num_nodes, sc->tris, tv, e1, e2, cones, g);
+      if (g_cluster_chord > 0 || cones.sup.size() * 10 <= cs.sup.size() * 14) cs = std::move(cones);
+    }
   }
   leaf_cl = cs.leaf_cl;
   leaf_sp = cs.leaf_sp;
@@ -2166,6 +2181,9 @@ int build_clusters(kdpt_ctx* c, const kdpt_scene* sc, const std::vector<float4>&
   c->S.num_supers = cs.supers_finite ? (int)sp.size() : 0;
   c->S.leaf_cl = dl;
   c->S.num_clusters = (int)info.size();
+  c->S.cl_counts = 0;
+  for (int i = 0; i < sc->num_nodes; i++)
+    if (leaf_cl[i].y != 0 && leaf_cl[i].y != (sc->nodes[i].triIdSize + CLUSTER - 1) / CLUSTER) c->S.cl_counts = 1;
   c->S.cl_info = di;
   c->S.cl_lo = dlo;
   c->S.cl_hi = dhi;
@@ -2468,8 +2486,8 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
     return rc;
   };
   if (hipSetDevice(device) != hipSuccess) return bail(fail(KDPT_ERR_HIP, "hipSetDevice failed"));
-  if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess)
-    return bail(fail(KDPT_ERR_HIP, "hipStreamCreate failed"));
+  c->cu_mask_streams = g_cu_mask_streams;
+  if (create_stream(c, &c->stream) != KDPT_OK) return bail(fail(KDPT_ERR_HIP, "hipStreamCreate failed"));
   int rc;
   // geoms / materials (viz_kd: the KD node boxes follow the analytic geoms, as boxes with the last material,
   // src/pathtrace.cu:1813-1831)
@@ -2704,7 +2722,6 @@ int kdpt_create(const kdpt_scene* sc, const kdpt_options* opt, int device, kdpt_
   HIP_TRY(hipDeviceSynchronize());
   if ((rc = kdpt_reset(c))) return bail(rc);
   c->reduce_spin_us = g_reduce_spin_us;
-  c->cu_mask_streams = g_cu_mask_streams;
   c->create_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t_create).count();
   *out = c;
   return KDPT_OK;

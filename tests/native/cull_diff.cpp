@@ -405,7 +405,14 @@ int main(int argc, char** argv) {
     return sim(argv[3], nodes.data(), nn, tris.data(), nt, tv, e1, e2, grp);
   }
   ClusterSet cs;
-  build_cluster_set(nodes.data(), nn, tris.data(), tv, e1, e2, cs);
+  // CLUSTER_CHORD > 0: the normal-cone grouping kdpt_create uses for meshes with a rigorous margin
+  // (kdpt_runtime.hip build_clusters, CLUSTER_CHORD_EXACT)
+  ClusterGrouping grouping;
+  if (getenv("CLUSTER_CHORD") && atof(getenv("CLUSTER_CHORD")) > 0) {
+    grouping.mode = 1;
+    grouping.chord = atof(getenv("CLUSTER_CHORD"));
+  }
+  build_cluster_set(nodes.data(), nn, tris.data(), tv, e1, e2, cs, grouping);
   std::vector<float4> clo, chi;
   build_chunk_boxes(tv, e1, e2, nt, clo, chi);
   const CullMargin cm = cluster_margin(cs.cv0, cs.ce1, cs.ce2);

@@ -93,6 +93,16 @@ def test_c5_margin_is_rigorous_and_never_drops_a_pass(cull_diff, trees):
     assert r["pass"] > 100_000  # the generators do produce u/v passes near the culled region
 
 
+def test_c5_normal_cone_clusters_never_drop_a_pass(cull_diff, trees):
+    """The clusters kdpt_create builds for C5's icosphere (normal cones of chord CLUSTER_CHORD_EXACT = 0.03 before
+    the Morton runs, kdpt_runtime.hip build_clusters): other clusters, supers, slabs and oriented boxes, the same
+    rigorous margin -- 3 * 10^6 adversarial lines find no dropped pass at any level."""
+    r = run(cull_diff, trees("icosphere_8"), 3_000_000, 42, env={"CLUSTER_CHORD": "0.03"})
+    assert r["exact"] == 1 and r["margin"] >= r["rigorous"], r
+    assert r["violations"] == 0, r
+    assert r["pass"] > 30_000, r
+
+
 @pytest.mark.parametrize("mesh", ["dragon_5", "icosphere_7"])
 def test_rigorous_margin_never_drops_a_pass(cull_diff, trees, mesh):
     """Meshes whose rigorous margin is above the cap (so the kernels use the masked cull's box coefficient 1e-3):
