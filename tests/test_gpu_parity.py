@@ -396,3 +396,30 @@ def test_derived_box_tree_in_lds(kdpt, oracle, mesh, level, knobs, want):
     ref, _ = oracle.OracleScene.from_description(desc).render(1, 3)
     for f, im in imgs.items():
         assert np.array_equal(im.view(np.uint32), ref.view(np.uint32)), f
+
+
+def test_process_knobs_keep_parity(kdpt):
+    """The process-wide knobs (kdpt_set_tuning(NULL, ...): defaults of contexts created afterwards) change the
+    cluster layout and the stream kind only: plain streams instead of CU-masked ones, Morton-run clusters or
+    normal cones of another chord give the default route's bits -- on the C5 mesh family (icosphere_8, whose
+    margin is rigorous, so its default is normal cones) and on dragon_5 with pipelined iterations."""
+    from kdtreepathtraceroptimization_amd.runtime import set_process_tuning
+    cases = [("icosphere_8", (48, 40), 16, 16), ("dragon_5", (96, 80), 8, 8)]
+    try:
+        for mesh, res, depth, cap in cases:
+            sd = kdpt.SceneData.from_description(load_fixture_scene("cornell", mesh, res=res, depth=depth))
+            imgs = []
+            for knobs in ({}, {"cu_mask_streams": 0}, {"cluster_chord": 0}, {"cluster_chord": 0.1}):
+                for k, v in knobs.items():
+                    set_process_tuning(k, v)
+                with kdpt.PathTracer(sd, kdpt.default_options(bounce_cap=cap)) as pt:
+                    pt.trace_iterations(1, 8, pipeline=2, batch=4)
+                    pt.synchronize()
+                    imgs.append(pt.image().copy())
+                set_process_tuning("cu_mask_streams", 1)
+                set_process_tuning("cluster_chord", -1)
+            for k in range(1, len(imgs)):
+                assert np.array_equal(imgs[k].view(np.uint32), imgs[0].view(np.uint32)), (mesh, k)
+    finally:
+        set_process_tuning("cu_mask_streams", 1)
+        set_process_tuning("cluster_chord", -1)
