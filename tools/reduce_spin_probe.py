@@ -55,15 +55,20 @@ def per_frame_ctx(pt, spin):
     return round(1e3 * (ts[1] - ts[0]) / (n1 - n0), 3)
 
 
-def per_frame_sharded(spin):
+def per_frame_sharded(spin, repeats=3):
+    # each call creates and destroys its two contexts: the per-frame time is the difference of two frame counts,
+    # the median of a few repeats (the creation's cost varies from call to call)
     assert lib.kdpt_set_tuning(None, b"reduce_spin_us", C.c_double(spin)) == 0, lib.kdpt_last_error()
-    ts = []
-    for n in (n0, n1):
-        t = time.perf_counter()
-        kdpt.render_sharded(sd, [0, 0], 0, n, a.spp, options=opt, pipeline=8, batch=16, reduce=kdpt.REDUCE_COPY)
-        ts.append(time.perf_counter() - t)
+    per = []
+    for _ in range(repeats):
+        ts = []
+        for n in (n0, 2 * n1):
+            t = time.perf_counter()
+            kdpt.render_sharded(sd, [0, 0], 0, n, a.spp, options=opt, pipeline=8, batch=16, reduce=kdpt.REDUCE_COPY)
+            ts.append(time.perf_counter() - t)
+        per.append(1e3 * (ts[1] - ts[0]) / (2 * n1 - n0))
     assert lib.kdpt_set_tuning(None, b"reduce_spin_us", C.c_double(0.0)) == 0
-    return round(1e3 * (ts[1] - ts[0]) / (n1 - n0), 3)
+    return round(sorted(per)[len(per) // 2], 3)
 
 
 lib.kdpt_set_tuning.argtypes = [C.c_void_p, C.c_char_p, C.c_double]
