@@ -357,7 +357,8 @@ def main():
                    "scene": args.scene, "mesh": args.mesh, "resolution": [W, H], "depth": args.depth,
                    "bounce_cap": args.bounce_cap, "spp_per_frame": F, "spp_per_gpu_per_frame": per_gpu,
                    "kd_nodes": sd.view.num_nodes, "kd_tri_refs": sd.view.num_tris,
-                   "intersect": pt.trace_config(),
+                   "intersect": {**pt.trace_config(), "create_ms": round(pt.stats().create_ms, 2),
+                                 "mask_build_ms": round(pt.stats().mask_build_ms, 2)},
                    **({"tuning": args.tune} if args.tune else {}),
                    "parallelism": (f"spp-sharded x{world}, one framebuffer reduce per frame: "
                                    + ("RCCL ncclReduce inside libkdpt (kdpt_render_frames)"

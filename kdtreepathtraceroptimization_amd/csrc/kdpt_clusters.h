@@ -455,7 +455,7 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
 // lies on the face plane at |y| >= R, where radial projection is (1/R)-Lipschitz, so r_b = half diagonal / R.
 // So |N . d - N . d_b| <= r_b (+ 1e-6 for the float d's length).  Exactly degenerate triangles are in every mask
 // when |e1||e2| > 0.3 and in none otherwise (their float determinant stays below FLT_EPSILON).
-constexpr int DIR_MASK_N = 128;  // finest cube-map cells per face edge (6 n^2 buckets; dir_mask_resolution)
+constexpr int DIR_MASK_N = 256;  // finest cube-map cells per face edge (6 n^2 buckets; dir_mask_resolution)
 
 // Per cluster entry of the masked cull (structure of arrays, 64 entries per cluster; dir_mask_cell): the unit
 // normal and the two thresholds on x = N . d_b -- front when x - r <= beta, danger when also x + r >= dthr --
@@ -589,13 +589,15 @@ inline void build_entry_normals(const ClusterSet& cs, std::vector<float4>& out) 
   }
 }
 
-// The cube-map resolution of the masks: the finest of DIR_MASK_N, 64, 32, ... 4 cells per face edge whose masks
+// The cube-map resolution of the masks: the finest of DIR_MASK_N, 128, 64, ... 4 cells per face edge whose masks
 // (8 bytes per cluster and bucket) fit in `budget` bytes, else 2.  A danger mask holds the triangles whose plane
 // passes within the bucket's radius (plus a band of 17.5 u rho / (Kf - c)) of its directions, so its bit count
-// falls with the bucket size: on C3 (dragon_5, 181 clusters, 142 MB at 128) the masked cull measured 0.80 of the
-// fast-margin cull's rate at 32 cells and Kf = 1e-4, 0.88 at 128 cells and Kf = 1e-3 (profiles/r05_ab_log.md).
-inline int dir_mask_resolution(int ncl, size_t budget = (size_t)160 << 20) {
-  for (int n : {DIR_MASK_N, 64, 32, 16, 8, 4})
+// falls with the bucket size: on C3 (dragon_5, 181 clusters, 569 MB at 256) the danger items per path halve with
+// each doubling of the resolution and the rate rises by ~120 Mrays/s per item: 4 967 / 5 412 / 5 668 / 5 780 /
+// 5 839 Mrays/s at 16 / 32 / 64 / 128 / 256 cells (profiles/r06_ab_log.md, sessions r06j, r06k).  Device memory
+// is plentiful (288 GB); the budget keeps a scene of many clusters to a coarser table.
+inline int dir_mask_resolution(int ncl, size_t budget = (size_t)640 << 20) {
+  for (int n : {DIR_MASK_N, 128, 64, 32, 16, 8, 4})
     if ((size_t)ncl * 6 * n * n * 8 <= budget) return n;
   return 2;
 }

@@ -1605,16 +1605,20 @@ __device__ void trace_phase(const DevScene& S, const NodeSrc& nodes, const Clust
           const f3 ii = mk3(bpermute_f(invdir.x, own), bpermute_f(invdir.y, own), bpermute_f(invdir.z, own));
           unsigned long long nm = 0ull;  // the danger triangles danger_needs_test keeps
           if (m) {
-            const float D = box_miss(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
+            // one normal record per trip, the first requested before box_miss (the cluster box from LDS, the
+            // line's reciprocal from its lane), so that its latency overlaps it (profiles/r06_ab_log.md r06l/r06m:
+            // +1 % against two records per trip)
             const int e0 = c * 64;
-            while (m) {  // two normal records per trip: one round trip for both
-              const int k0 = __builtin_ctzll(m);
-              m &= m - 1;
-              const int k1 = m ? __builtin_ctzll(m) : k0;
-              m &= m - 1;
-              const float4 t0 = S.cl_tn[e0 + k0], t1 = S.cl_tn[e0 + k1];
+            int k0 = __builtin_ctzll(m);
+            m &= m - 1;
+            float4 t0 = S.cl_tn[e0 + k0];
+            const float D = box_miss(clusters.lo_of(c), clusters.hi_of(c), oo, ii);
+            while (true) {
               if (danger_needs_test(t0, dd, D, S.cull_c)) nm |= 1ull << k0;
-              if (danger_needs_test(t1, dd, D, S.cull_c)) nm |= 1ull << k1;
+              if (!m) break;
+              k0 = __builtin_ctzll(m);
+              m &= m - 1;
+              t0 = S.cl_tn[e0 + k0];
             }
           }
           if (__any(nm != 0ull)) {  // (rare) glm's u/v tests on the kept ones

@@ -2850,7 +2850,7 @@ int kdpt_set_tuning(kdpt_ctx* c, const char* name, double value) {
       int rc = build_masks(c, c->mask_n);
       if (rc) return rc;
     } else {
-      if (v < 1 || v > 128) return fail(KDPT_ERR_ARG, "cull_mask_n must be in 1 .. 128");
+      if (v < 1 || v > 512) return fail(KDPT_ERR_ARG, "cull_mask_n must be in 1 .. 512");
       if (!c->mask_cs) return fail(KDPT_ERR_ARG, "cull_mask_n: this scene has no direction masks");
       int rc = build_masks(c, v);
       if (rc) return rc;

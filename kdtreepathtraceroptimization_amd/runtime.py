@@ -519,6 +519,10 @@ class PathTracer:
                "lds_tree_bytes": l.value}
         if hasattr(self.lib, "kdpt_cull_margin"):
             out.update(self.cull_margin())
+        if hasattr(self.lib, "kdpt_cull_masks"):
+            n, ncl = C.c_int(), C.c_int()
+            _check(self.lib.kdpt_cull_masks(self._ctx, C.byref(n), C.byref(ncl), None), "kdpt_cull_masks")
+            out["cull_mask_n"] = n.value
         return out
 
     def cull_margin(self) -> dict:

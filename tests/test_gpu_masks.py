@@ -54,16 +54,17 @@ def _host_masks(cull_diff, sd, path, n=None):
 
 
 def test_device_masks_equal_host_builder(kdpt, cull_diff, tmp_path):
-    """dragon_5 (C3's mesh): the 6 * 128^2 * 181 cells the device builds equal the host builder's, bit for bit;
+    """dragon_5 (C3's mesh): the 6 * 256^2 * 181 cells the device builds equal the host builder's, bit for bit;
     most cells are empty."""
     desc = load_fixture_scene("cornell", "dragon_5", res=(64, 48), depth=8)
     sd = kdpt.SceneData.from_description(desc)
-    info, n, hm = _host_masks(cull_diff, sd, str(tmp_path / "m128.bin"))
+    info, n, hm = _host_masks(cull_diff, sd, str(tmp_path / "m256.bin"))
     with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
         dn, dm = pt.cull_masks()
-        assert dn == n == 128, (dn, info)
+        assert dn == n == 256, (dn, info)
         assert np.array_equal(dm, hm)
-        assert 0.1 < (dm != 0).mean() < 0.6, (dm != 0).mean()
+        assert 0.05 < (dm != 0).mean() < 0.6, (dm != 0).mean()
+        del hm
         assert pt.stats().mask_build_ms > 0
         # rebuilt by the knob at another resolution: still the host builder's cells
         pt.set_tuning("cull_mask_n", 32)
