@@ -28,6 +28,7 @@
 #include <algorithm>
 #include <chrono>
 #include <cstdint>
+#include <cstdio>
 #include <cstdlib>
 #include <cstring>
 #include <type_traits>
@@ -38,10 +39,14 @@
 
 namespace {
 
-#define KD_TRY(x)                                   \
-  do {                                              \
-    hipError_t e_ = (x);                            \
-    if (e_ != hipSuccess) return KDPT_ERR_HIP;      \
+// (the failing call and HIP's reason on stderr: the scene-build entry points return only the code)
+#define KD_TRY(x)                                                                                       \
+  do {                                                                                                  \
+    hipError_t e_ = (x);                                                                                \
+    if (e_ != hipSuccess) {                                                                             \
+      fprintf(stderr, "[kdpt] device KD build: %s failed: %s\n", #x, hipGetErrorString(e_));           \
+      return KDPT_ERR_HIP;                                                                              \
+    }                                                                                                   \
   } while (0)
 
 constexpr int BLK = 256;
