@@ -246,7 +246,7 @@ int kdpt_set_options(kdpt_ctx *ctx, const kdpt_options *opt);
  * construction), "cull_margin" (0 = the scene's; > 0 overrides the cull's margin coefficient, no masks),
  * "cull_exact" (1; 0 = for meshes of large triangles the margin-only cull instead of the masked exact one, not
  * exact), "cull_mask_n" (the direction masks' cube-map cells per face edge, 1 .. 512; default: the finest of
- * 512 / 256 / 128 ... within 2.5 GB), "cull_fast_k" (the masked cull's box coefficient, default 1e-3; the masks
+ * 256 / 128 / 64 ... within 640 MB), "cull_fast_k" (the masked cull's box coefficient, default 1e-3; the masks
  * are rebuilt for it), "reduce_spin_us" (0; > 0: a device spin of that many
  * microseconds on the reduce stream before every frame's reduce, emulating an ncclReduce that waits for a slower
  * peer -- a diagnostic of the frame pipeline; ctx = NULL sets it for contexts created later, e.g. the ones

@@ -455,7 +455,7 @@ inline void build_cluster_set(const kdpt_node_bare* nodes, int nn, const kdpt_tr
 // lies on the face plane at |y| >= R, where radial projection is (1/R)-Lipschitz, so r_b = half diagonal / R.
 // So |N . d - N . d_b| <= r_b (+ 1e-6 for the float d's length).  Exactly degenerate triangles are in every mask
 // when |e1||e2| > 0.3 and in none otherwise (their float determinant stays below FLT_EPSILON).
-constexpr int DIR_MASK_N = 512;  // finest cube-map cells per face edge (6 n^2 buckets; dir_mask_resolution)
+constexpr int DIR_MASK_N = 256;  // finest cube-map cells per face edge (6 n^2 buckets; dir_mask_resolution)
 
 // Per cluster entry of the masked cull (structure of arrays, 64 entries per cluster; dir_mask_cell): the unit
 // normal and the two thresholds on x = N . d_b -- front when x - r <= beta, danger when also x + r >= dthr --
@@ -509,8 +509,25 @@ inline void mask_entries(const ClusterSet& cs, float Kf, MaskEntries& me) {
 // The buckets' centre directions and radii (4 doubles per bucket, dir_mask_cell's D).
 inline void mask_buckets(int n, std::vector<double>& bd) {
   const int nb = 6 * n * n;
+  const double grow = 1e-5;
   bd.assign(4 * (size_t)nb, 0.0);
-  for (int b = 0; b < nb; b++) mask_bucket(n, b, &bd[4 * (size_t)b]);
+  for (int b = 0; b < nb; b++) {
+    const int face = b / (n * n), j = (b / n) % n, i = b % n;
+    const double a0 = -1.0 + 2.0 * i / n - grow, a1 = -1.0 + 2.0 * (i + 1) / n + grow;
+    const double b0 = -1.0 + 2.0 * j / n - grow, b1 = -1.0 + 2.0 * (j + 1) / n + grow;
+    const double ac = 0.5 * (a0 + a1), bc = 0.5 * (b0 + b1);
+    const double amin = (a0 <= 0 && a1 >= 0) ? 0.0 : std::min(std::fabs(a0), std::fabs(a1));
+    const double bmin = (b0 <= 0 && b1 >= 0) ? 0.0 : std::min(std::fabs(b0), std::fabs(b1));
+    const double R = std::sqrt(1.0 + amin * amin + bmin * bmin);
+    double* D = &bd[4 * (size_t)b];
+    D[3] = 0.5 * std::sqrt((a1 - a0) * (a1 - a0) + (b1 - b0) * (b1 - b0)) / R * (1.0 + 1e-9) + 1e-6;
+    const double sgn = (face & 1) ? -1.0 : 1.0;
+    if (face < 2) { D[0] = sgn; D[1] = ac; D[2] = bc; }
+    else if (face < 4) { D[0] = ac; D[1] = sgn; D[2] = bc; }
+    else { D[0] = ac; D[1] = bc; D[2] = sgn; }
+    const double dl = std::sqrt(D[0] * D[0] + D[1] * D[1] + D[2] * D[2]);
+    for (int a = 0; a < 3; a++) D[a] /= dl;
+  }
 }
 
 // The masks on the host, bucket-major (masks[b ncl + c]: DevScene::cl_mask).  Test infrastructure: the product
@@ -572,16 +589,15 @@ inline void build_entry_normals(const ClusterSet& cs, std::vector<float4>& out) 
   }
 }
 
-// The cube-map resolution of the masks: the finest of DIR_MASK_N, 256, 128, ... 4 cells per face edge whose masks
+// The cube-map resolution of the masks: the finest of DIR_MASK_N, 128, 64, ... 4 cells per face edge whose masks
 // (8 bytes per cluster and bucket) fit in `budget` bytes, else 2.  A danger mask holds the triangles whose plane
 // passes within the bucket's radius (plus a band of 17.5 u rho / (Kf - c)) of its directions, so its bit count
-// falls with the bucket size: on C3 (dragon_5, 181 clusters, 2.3 GB at 512) the danger items per path halve with
+// falls with the bucket size: on C3 (dragon_5, 181 clusters, 569 MB at 256) the danger items per path halve with
 // each doubling of the resolution and the rate rises by ~120 Mrays/s per item: 4 967 / 5 412 / 5 668 / 5 780 /
-// 5 839 Mrays/s at 16 / 32 / 64 / 128 / 256 cells (profiles/r06_ab_log.md, sessions r06j, r06k), and 512 cells
-// measured +1.0 % over 256 (r06x).  Device memory is plentiful (288 GB); the budget keeps a scene of many
-// clusters to a coarser table.
-inline int dir_mask_resolution(int ncl, size_t budget = (size_t)2560 << 20) {
-  for (int n : {DIR_MASK_N, 256, 128, 64, 32, 16, 8, 4})
+// 5 839 Mrays/s at 16 / 32 / 64 / 128 / 256 cells (profiles/r06_ab_log.md, sessions r06j, r06k).  Device memory
+// is plentiful (288 GB); the budget keeps a scene of many clusters to a coarser table.
+inline int dir_mask_resolution(int ncl, size_t budget = (size_t)640 << 20) {
+  for (int n : {DIR_MASK_N, 128, 64, 32, 16, 8, 4})
     if ((size_t)ncl * 6 * n * n * 8 <= budget) return n;
   return 2;
 }

@@ -676,30 +676,6 @@ KDPT_HD bool danger_needs_test(float4 tn, f3 d, float D, float c) {
 // direction-free rigorous coefficient K_t = 8.75 |e1||e2| + c exceeds Kf (a line glm's float u/v tests accept for
 // t passes within K_t W of any region holding t -- DESIGN.md 4, "Cluster cull" -- so a pair that missed the box
 // or the oriented box at Kf >= K_t cannot need t).
-// Bucket b of the masks' cube map at n cells per face edge (face-major, then row j, column i): its centre direction
-// D[0..2] (unit, double) and a rigorous radius D[3] over its directions, the cell grown by 1e-5 on the face plane
-// (|y| >= R there, where radial projection is (1/R)-Lipschitz).  IEEE double operations only (+, -, *, /, sqrt),
-// so the host builder (kdpt_clusters.h mask_buckets) and k_build_masks get the same bits.
-KDPT_HD void mask_bucket(int n, int b, double* D) {
-  const double grow = 1e-5;
-  const int face = b / (n * n), j = (b / n) % n, i = b % n;
-  const double a0 = -1.0 + 2.0 * i / n - grow, a1 = -1.0 + 2.0 * (i + 1) / n + grow;
-  const double b0 = -1.0 + 2.0 * j / n - grow, b1 = -1.0 + 2.0 * (j + 1) / n + grow;
-  const double ac = 0.5 * (a0 + a1), bc = 0.5 * (b0 + b1);
-  const double fa0 = a0 < 0.0 ? -a0 : a0, fa1 = a1 < 0.0 ? -a1 : a1;
-  const double fb0 = b0 < 0.0 ? -b0 : b0, fb1 = b1 < 0.0 ? -b1 : b1;
-  const double amin = (a0 <= 0 && a1 >= 0) ? 0.0 : (fa1 < fa0 ? fa1 : fa0);
-  const double bmin = (b0 <= 0 && b1 >= 0) ? 0.0 : (fb1 < fb0 ? fb1 : fb0);
-  const double R = sqrt(1.0 + amin * amin + bmin * bmin);
-  D[3] = 0.5 * sqrt((a1 - a0) * (a1 - a0) + (b1 - b0) * (b1 - b0)) / R * (1.0 + 1e-9) + 1e-6;
-  const double sgn = (face & 1) ? -1.0 : 1.0;
-  if (face < 2) { D[0] = sgn; D[1] = ac; D[2] = bc; }
-  else if (face < 4) { D[0] = ac; D[1] = sgn; D[2] = bc; }
-  else { D[0] = ac; D[1] = bc; D[2] = sgn; }
-  const double dl = sqrt(D[0] * D[0] + D[1] * D[1] + D[2] * D[2]);
-  for (int a = 0; a < 3; a++) D[a] /= dl;
-}
-
 KDPT_HD unsigned long long dir_mask_cell(const double* nx, const double* ny, const double* nz, const double* beta,
                                          const double* dthr, const float* krig, const double* D, float Kf) {
   unsigned long long md = 0ull;

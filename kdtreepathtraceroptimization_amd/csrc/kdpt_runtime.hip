@@ -2022,7 +2022,7 @@ void apply_cull_route(kdpt_ctx* c) {
 // workgroup per (cluster, 256 buckets), the cluster's 64 entries staged in LDS (every lane reads the same entry:
 // a broadcast), one mask per lane, written bucket-major.
 __global__ void __launch_bounds__(256) k_build_masks(const double* __restrict__ ent, const float* __restrict__ krig,
-                                                     int n, int ncl, int nb, float Kf,
+                                                     const double* __restrict__ bd, int ncl, int nb, float Kf,
                                                      unsigned long long* __restrict__ masks) {
   __shared__ double se[5][64];
   __shared__ float sk[64];
@@ -2035,9 +2035,7 @@ __global__ void __launch_bounds__(256) k_build_masks(const double* __restrict__ 
   __syncthreads();
   const int b = blockIdx.y * 256 + threadIdx.x;
   if (b >= nb) return;
-  double D[4];
-  mask_bucket(n, b, D);  // (recomputed per cluster: cheaper than uploading 32 bytes per bucket)
-  masks[(size_t)b * ncl + c] = dir_mask_cell(se[0], se[1], se[2], se[3], se[4], sk, D, Kf);
+  masks[(size_t)b * ncl + c] = dir_mask_cell(se[0], se[1], se[2], se[3], se[4], sk, bd + 4 * (size_t)b, Kf);
 }
 
 // Release one of the context's device allocations before kdpt_destroy (a rebuilt table).
@@ -2048,9 +2046,8 @@ void dfree(kdpt_ctx* c, void* p) {
   (void)hipFree(p);
 }
 
-// The direction masks of the scene's clusters at resolution n (cube-map cells per face edge), built on the device
-// (k_build_masks) from the per-entry records the host computes (kdpt_clusters.h mask_entries) and the buckets'
-// geometry (kdpt_device.h mask_bucket, computed in the kernel; tests/test_gpu_masks.py checks the cells against the
+// The direction masks of the scene's clusters at resolution n (cube-map cells per face edge), built on the device (k_build_masks) from the per-entry records and the bucket directions the host
+// computes (kdpt_clusters.h mask_entries / mask_buckets; tests/test_gpu_parity.py checks the cells against the
 // host builder).  A rebuild (knobs "cull_mask_n", "cull_fast_k") frees the previous tables.
 int build_masks(kdpt_ctx* c, int n) {
   const auto t0 = std::chrono::steady_clock::now();
@@ -2059,6 +2056,8 @@ int build_masks(kdpt_ctx* c, int n) {
   const float Kf = c->cull.K;
   MaskEntries me;
   mask_entries(cs, Kf, me);
+  std::vector<double> bd;
+  mask_buckets(n, bd);
   const size_t ne = 64 * (size_t)ncl;
   std::vector<double> ent(5 * ne);
   for (size_t k = 0; k < ne; k++) {
@@ -2077,23 +2076,27 @@ int build_masks(kdpt_ctx* c, int n) {
   c->mask_dev = dm;
   double* d_ent = nullptr;
   float* d_krig = nullptr;
+  double* d_bd = nullptr;
   auto release = [&]() {
     (void)hipFree(d_ent);
     (void)hipFree(d_krig);
+    (void)hipFree(d_bd);
   };
   // (the uploads on the context's stream, ahead of the kernel; pageable sources are staged before each call
   // returns, and the stream is drained before the temporaries go)
   if (hipMalloc(&d_ent, ent.size() * sizeof(double)) != hipSuccess ||
       hipMalloc(&d_krig, me.krig.size() * sizeof(float)) != hipSuccess ||
+      hipMalloc(&d_bd, bd.size() * sizeof(double)) != hipSuccess ||
       hipMemcpyAsync(d_ent, ent.data(), ent.size() * sizeof(double), hipMemcpyHostToDevice, c->stream) != hipSuccess ||
       hipMemcpyAsync(d_krig, me.krig.data(), me.krig.size() * sizeof(float), hipMemcpyHostToDevice, c->stream) !=
-          hipSuccess) {
+          hipSuccess ||
+      hipMemcpyAsync(d_bd, bd.data(), bd.size() * sizeof(double), hipMemcpyHostToDevice, c->stream) != hipSuccess) {
     (void)hipStreamSynchronize(c->stream);
     release();
     return fail(KDPT_ERR_HIP, "mask build: device buffers");
   }
-  hipLaunchKernelGGL(k_build_masks, dim3(ncl, (nb + 255) / 256), dim3(256), 0, c->stream, d_ent, d_krig, n, ncl, nb,
-                     Kf, dm);
+  hipLaunchKernelGGL(k_build_masks, dim3(ncl, (nb + 255) / 256), dim3(256), 0, c->stream, d_ent, d_krig, d_bd, ncl,
+                     nb, Kf, dm);
   const hipError_t e1 = hipGetLastError(), e2 = hipStreamSynchronize(c->stream);
   release();
   if (e1 != hipSuccess || e2 != hipSuccess) return fail(KDPT_ERR_HIP, "k_build_masks failed");

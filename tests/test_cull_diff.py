@@ -141,7 +141,7 @@ def test_direction_masks_never_drop_a_pass(cull_diff, trees, mesh, n):
     margin is above the cap): for every adversarial line that misses a cluster's box or oriented box at the box
     coefficient, every triangle that passes glm's u/v tests is among those the kernel still tests -- the danger
     mask holds the triangle and danger_needs_test keeps it -- with the reciprocal of dir_bucket / box_miss moved by
-    -1, 0 and +1 ulp, at several cube-map resolutions including the shipped 512 cells."""
+    -1, 0 and +1 ulp, at several cube-map resolutions including the shipped 256 cells and 512."""
     r = run(cull_diff, trees(mesh), 3_000_000 if mesh == "dragon_5" else 1_000_000, 53 + n, env={"MASK_N": str(n)})
     assert r["viol_mask"] == 0, r
     assert r["pass"] > 50_000, r
@@ -152,7 +152,7 @@ def test_direction_masks_never_drop_a_pass(cull_diff, trees, mesh, n):
 def test_real_rays_through_the_traversal_keep_every_pass(cull_diff, trees, rays_c3, n):
     """Rays of a real C3 render walked through the traversal (tests/native/cull_diff.cpp --sim): at every big
     leaf they visit, every cluster triangle that passes glm's u/v tests is swept or tested by the masked cull
-    (under the three reciprocal perturbations), at the shipped 512 cells, at 256, 128 and 32; the masked cull tests
+    (under the three reciprocal perturbations), at the shipped 256 cells, at 512, 128 and 32; the masked cull tests
     about as many triangles per ray as the fast one swept (no perf cliff: at most 1.5x); from 128 cells up most
     missed pairs' masks are empty."""
     r = run(cull_diff, trees("dragon_5"), "--sim", rays_c3, 0, env={"MASK_N": str(n)})

@@ -54,16 +54,16 @@ def _host_masks(cull_diff, sd, path, n=None):
 
 
 def test_device_masks_equal_host_builder(kdpt, cull_diff, tmp_path):
-    """dragon_5 (C3's mesh): the 6 * 512^2 * 181 cells the device builds equal the host builder's, bit for bit;
+    """dragon_5 (C3's mesh): the 6 * 256^2 * 181 cells the device builds equal the host builder's, bit for bit;
     most cells are empty."""
     desc = load_fixture_scene("cornell", "dragon_5", res=(64, 48), depth=8)
     sd = kdpt.SceneData.from_description(desc)
-    info, n, hm = _host_masks(cull_diff, sd, str(tmp_path / "m512.bin"))
+    info, n, hm = _host_masks(cull_diff, sd, str(tmp_path / "m256.bin"))
     with kdpt.PathTracer(sd, kdpt.default_options()) as pt:
         dn, dm = pt.cull_masks()
-        assert dn == n == 512, (dn, info)
+        assert dn == n == 256, (dn, info)
         assert np.array_equal(dm, hm)
-        assert 0.02 < (dm != 0).mean() < 0.6, (dm != 0).mean()
+        assert 0.05 < (dm != 0).mean() < 0.6, (dm != 0).mean()
         del hm
         assert pt.stats().mask_build_ms > 0
         # rebuilt by the knob at another resolution: still the host builder's cells
@@ -95,8 +95,7 @@ def test_mask_rebuilds_free_the_previous_tables(kdpt):
 def test_create_time_on_c3(kdpt):
     """kdpt_create on C3 (cornell + dragon_5, 800x800, depth 8) with the masks built on the device: the host
     wall time kdpt_stats reports for a context created after the process's first (as the shim re-creates one on
-    every camera move) stays within 50 ms (measured 28-30 ms at 512 cells, of which the masks 11.5), and the masks
-    take a small part
+    every camera move) stays within 50 ms (measured 4-5 ms, of which the masks 2.4), and the masks take a small part
     of it."""
     desc = load_fixture_scene("cornell", "dragon_5", res=(800, 800), depth=8)
     sd = kdpt.SceneData.from_description(desc)
